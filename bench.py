@@ -1,0 +1,195 @@
+#!/usr/bin/env python3
+"""Benchmark: utterances/sec of PESQ-wb + STOI/ESTOI on 10 s @ 16 kHz pairs (BASELINE.json).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--length L]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+One step = the drop-in API calls ``PESQ(16000, use_gpu=True)(clean, noisy)`` and
+``STOI(16000, use_gpu=True)(clean, noisy)`` on this rank's batch (4096 pairs per GPU by
+default: BASELINE.json configs[1], 10 s @ 16 kHz fp32), including the list-of-dict result
+construction, plus (N > 1) the RCCL all-gather of the per-utterance scores over xGMI.
+Weak scaling: every rank owns its own shard of utterances, generated in HBM before timing.
+
+Rank 0 prints ONE JSON line with the metric, the roofline of the dominant kernel
+(pesq_front: algorithmic bytes / its HIP-event-timed duration vs 8 TB/s) and the CPU
+baseline (the oracle CPU restatement on a bounded sample, single core).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+METRIC = "utterances/sec PESQ-wb+STOI, 10s@16kHz, batch 4096, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=4096, help="utterance pairs per GPU")
+    ap.add_argument("--length", type=int, default=160000, help="samples per utterance (16 kHz)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--kernel-reps", type=int, default=5)
+    return ap.parse_args()
+
+
+def cpu_baseline(clean, noisy, budget_s):
+    """Oracle CPU restatement (oracle/), one core, on a bounded sample of the same workload."""
+    try:
+        from threadpoolctl import threadpool_limits
+    except Exception:  # pragma: no cover
+        threadpool_limits = None
+    from oracle import pesq_oracle, stoi_oracle
+
+    ctx = threadpool_limits(limits=1) if threadpool_limits else None
+    torch_threads = torch.get_num_threads()
+    torch.set_num_threads(1)
+    n = 0
+    t0 = time.perf_counter()
+    try:
+        if ctx:
+            ctx.__enter__()
+        while True:
+            c = clean[n:n + 1].cpu().numpy()
+            d = noisy[n:n + 1].cpu().numpy()
+            pesq_oracle.pesq(c, d)
+            stoi_oracle.stoi(c, d, 16000)
+            n += 1
+            if time.perf_counter() - t0 >= budget_s or n >= clean.shape[0]:
+                break
+    finally:
+        if ctx:
+            ctx.__exit__(None, None, None)
+        torch.set_num_threads(torch_threads)
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "utterances/s", "cores": 1, "kind": "port",
+            "sample": f"{n} pairs x {clean.shape[1]} samples @16kHz, PESQ-wb + STOI/ESTOI, "
+                      f"oracle numpy/C restatement, {dt:.1f} s"}
+
+
+def kernel_roofline(pesq, clean, noisy, reps):
+    """HIP-event timing of the dominant kernel (pesq_front via fsem_pesq_front_f32) on the
+    stream it is launched on; achieved = algorithmic bytes per launch / avg duration."""
+    from fast_speech_enhancement_metrics_amd import _native
+    lib = _native.load()
+    B, L = clean.shape
+    F = lib.fsem_pesq_frames(L)
+    dev = clean.device
+    bark = torch.empty(2 * B, F, 49, device=dev)
+    power = torch.empty(2 * B, device=dev)
+    ws = _native.workspace(lib.fsem_pesq_front_workspace_bytes(B, L), dev)
+    stream = torch.cuda.current_stream(dev)
+    h = stream.cuda_stream
+
+    def launch():
+        _native.check(lib.fsem_pesq_front_f32(clean.data_ptr(), noisy.data_ptr(), B, L, L, bark.data_ptr(),
+                                              power.data_ptr(), ws.data_ptr(), ws.numel(), h), "front")
+
+    launch()
+    torch.cuda.synchronize(dev)
+    start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    start.record(stream)
+    for _ in range(reps):
+        launch()
+    end.record(stream)
+    end.synchronize()
+    ms = start.elapsed_time(end) / reps
+    algo_bytes = 2 * B * L * 4  # both signals read once (2*L*4 B per pair)
+    achieved = algo_bytes / (ms * 1e-3) / 1e9
+    return {"kernel": "pesq_front", "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "ms_per_launch": round(ms, 4), "algorithmic_bytes_per_launch": algo_bytes}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    distributed = world > 1
+    if distributed:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from fast_speech_enhancement_metrics_amd import PESQ, STOI
+    from fast_speech_enhancement_metrics_amd.synthetic import speech_like_pairs
+
+    B, L = args.batch, args.length
+    clean, noisy, _ = speech_like_pairs(B, L, 16000, seed=42 + rank, device=dev)
+    torch.cuda.synchronize(dev)
+    pesq = PESQ(16000, use_gpu=True)
+    stoi = STOI(16000, use_gpu=True)
+
+    gather_buf = None
+    if distributed:
+        gather_buf = torch.empty(world * B, 3, device=dev)
+
+    def step():
+        r_p = pesq(clean, noisy)
+        r_s = stoi(clean, noisy)
+        if distributed:
+            mine = torch.tensor([[a["PESQ"], b["STOI"], b["ESTOI"]] for a, b in zip(r_p, r_s)],
+                                dtype=torch.float32).to(dev, non_blocking=True)
+            dist.all_gather_into_tensor(gather_buf, mine)
+        return r_p, r_s
+
+    for _ in range(args.warmup):
+        step()
+
+    def barrier():
+        if distributed:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    dt = time.perf_counter() - t0
+    if distributed:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    ms_per_step = dt / args.steps * 1e3
+    value = world * B * args.steps / dt
+
+    roof = kernel_roofline(pesq, clean, noisy, args.kernel_reps)
+    out = None
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(clean, noisy, args.cpu_seconds)
+        out = {
+            "metric": METRIC, "value": round(value, 2), "unit": "utterances/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (speech-like harmonic source + AM noise, SNR U[-5,25] dB, int16 grid)",
+            "config": {"workload": "PESQ-wb + STOI/ESTOI drop-in API calls, 10 s @ 16 kHz fp32 pairs",
+                       "batch_per_gpu": B, "global_batch": world * B, "length": L, "sample_rate": 16000,
+                       "parallelism": f"dp{world} (utterance shards, RCCL all-gather of scores)"},
+            "roofline": roof, "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if distributed:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,8 @@
+"""Drop-in import path of the reference package: ``from fast_se_metrics import PESQ, STOI``.
+
+Only the hot-path metrics (PESQ-wb, STOI/ESTOI) are provided; SDR, LSD, DNSMOS and
+SpeechBERTScore of the reference are out of scope.
+"""
+from fast_speech_enhancement_metrics_amd import PESQ, STOI  # noqa: F401
+
+__all__ = ["STOI", "PESQ"]

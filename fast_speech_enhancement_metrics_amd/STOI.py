@@ -1,0 +1,83 @@
+"""STOI / ESTOI metric -- drop-in for the reference's ``fast_se_metrics.STOI`` (STOI.py:7-205).
+
+Runs at 10 kHz internally (STOI.py:9).  ``use_gpu=True``: libfsem's gfx950 kernels
+(``fsem_stoi_f32``) with the 16 -> 10 kHz resampler fused into them (the reference
+resamples in BaseMetric.prepare_audio, base.py:19-20; same arithmetic), one device->host
+copy of the scores.  ``use_gpu=False``: the package's CPU implementation.
+"""
+from __future__ import annotations
+
+import warnings
+
+import torch
+
+from . import _cpu, _native
+from .base import BaseMetric, as_rows
+
+
+class STOI(BaseMetric):
+    higher_is_better = True
+    EXPECTED_SAMPLING_RATE = 10000
+
+    def __init__(self, sample_rate: int = 10000, use_gpu: bool = False):
+        super().__init__(sample_rate, use_gpu)
+        self.sampling_frequency = self.EXPECTED_SAMPLING_RATE
+        self.win_length = 256
+        self.hop_length = self.win_length // 2
+        self.n_fft = 512
+        self.num_octave_bands = 15
+        self.min_frequency = 150
+        self.N = 30
+        self.beta = -15.0
+        self.dynamic_range = 40
+
+    def scores(self, clean_speech: torch.Tensor, denoised_speech: torch.Tensor, sample_rate: int | None = None):
+        """(stoi[B], estoi[B]) tensors on the metric's device; NaN where no segment exists."""
+        sr = self.EXPECTED_SAMPLING_RATE if sample_rate is None else int(sample_rate)
+        clean = as_rows(clean_speech)
+        noisy = as_rows(denoised_speech)
+        if noisy.shape != clean.shape:
+            raise Exception("`clean_speech` and `denoised_speech` should have the same shape.")
+        B, L = clean.shape
+        if not clean.is_cuda:
+            if sr != self.EXPECTED_SAMPLING_RATE:
+                clean, noisy = self.resampler(clean), self.resampler(noisy)
+            return _cpu.stoi(clean, noisy)
+        lib = _native.load()
+        if clean.stride(0) != noisy.stride(0):
+            clean, noisy = clean.contiguous(), noisy.contiguous()
+        s = torch.empty(B, dtype=torch.float32, device=clean.device)
+        e = torch.empty(B, dtype=torch.float32, device=clean.device)
+        nbytes = lib.fsem_stoi_workspace_bytes(B, L, sr)
+        if nbytes == 0:
+            raise NotImplementedError(f"unsupported sample rate {sr} for the fused STOI resampler")
+        ws = _native.workspace(nbytes, clean.device)
+        rc = lib.fsem_stoi_f32(clean.data_ptr(), noisy.data_ptr(), B, L, clean.stride(0), sr, s.data_ptr(),
+                               e.data_ptr(), ws.data_ptr(), ws.numel(), _native.stream_handle(clean.device))
+        if rc == _native.FSEM_ESHORT:
+            raise RuntimeError("STOI input shorter than one 256-sample frame at 10 kHz")
+        _native.check(rc, "STOI")
+        return s, e
+
+    def _finish(self, stois: torch.Tensor, estois: torch.Tensor) -> list[dict[str, float]]:
+        s, e = torch.stack([stois.float(), estois.float()]).tolist()
+        if all(x != x for x in s):  # no utterance has a 30-frame segment (STOI.py:162-165)
+            warnings.warn("Not enough non-silent frames. Please check your sound files", RuntimeWarning, stacklevel=3)
+            raise TypeError("iteration over a 0-d tensor")
+        return [{"STOI": a, "ESTOI": b} for a, b in zip(s, e)]
+
+    def compute_metric(self, clean_speech: torch.Tensor | None, denoised_speech: torch.Tensor) -> list[dict[str, float]]:
+        assert clean_speech is not None
+        with torch.no_grad():
+            return self._finish(*self.scores(clean_speech, denoised_speech))
+
+    def __call__(self, clean_speech: torch.Tensor | None, denoised_speech: torch.Tensor) -> list[dict[str, float]]:
+        if self.device == "cuda" and clean_speech is not None:
+            # GPU: resampling is fused into the STOI kernels -- skip BaseMetric's resampler
+            if clean_speech.shape != denoised_speech.shape:
+                raise Exception("`clean_speech` and `denoised_speech` should have the same shape.")
+            clean = torch.atleast_2d(clean_speech).to(self.device)
+            noisy = torch.atleast_2d(denoised_speech).to(self.device)
+            with torch.no_grad():
+                return self._finish(*self.scores(clean, noisy, self.sample_rate))
+        return super().__call__(clean_speech, denoised_speech)

@@ -1,0 +1,11 @@
+"""MI355X-native batched PESQ-wb and STOI/ESTOI (drop-in for kcoost/fast_speech_enhancement_metrics).
+
+    from fast_speech_enhancement_metrics_amd import PESQ, STOI
+    PESQ(sample_rate=16000, use_gpu=True)(clean, denoised)  -> [{"PESQ": ...}, ...]
+    STOI(sample_rate=16000, use_gpu=True)(clean, denoised)  -> [{"STOI": ..., "ESTOI": ...}, ...]
+"""
+from .base import BaseMetric
+from .PESQ import PESQ
+from .STOI import STOI
+
+__all__ = ["BaseMetric", "PESQ", "STOI"]

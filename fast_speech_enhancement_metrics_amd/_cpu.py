@@ -1,0 +1,165 @@
+"""CPU mode of the metrics (``use_gpu=False``), the reference's CPU behaviour.
+
+Batched torch/scipy implementation of the same math the HIP engine runs:
+  PESQ: fast_se_metrics/PESQ.py:92-245, utils/bark.py:169-204, utils/loudness.py:48-67
+  STOI: fast_se_metrics/STOI.py:26-205
+The level-alignment band-pass runs as a float64 second-order-section cascade and the
+pre-emphasis as a float64 IIR (scipy C loops); spectra via torch.stft.  STOI's
+``normalize`` is deterministic here (no 1e-12 * randn term; zero-variance rows map to 0).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+from scipy.signal import butter, lfilter, sosfilt, tf2zpk, zpk2sos
+
+from . import _tables as T
+
+# ----------------------------------------------------------------------------- PESQ constants
+_NB = 49
+_EDGES = np.concatenate([[0], np.cumsum(T.BINS_PER_BAND)])
+_FBANK = torch.zeros(_NB, 256, dtype=torch.float64)
+for _i in range(_NB):
+    _FBANK[_i, _EDGES[_i]:_EDGES[_i + 1]] = 1.0
+_CORR = torch.tensor(T.POW_DENS_CORRECTION, dtype=torch.float64) * T.SP_16K
+_THR = torch.tensor(T.ABS_THRESH_POWER, dtype=torch.float64)
+_EXP = ((6 / (torch.tensor(T.CENTRE_BARK) + 2.0)).clamp(1.0, 2.0) ** 0.15 * T.ZWICKER_POWER).to(torch.float64)
+_WB = torch.tensor(T.WIDTH_BARK, dtype=torch.float64)
+_TW = float(_WB[1:].sum())
+_bb, _ba = butter(5, [325, 3250], fs=16000, btype="band")
+_BP_B = np.asarray(_bb, dtype=np.float32).astype(np.float64)
+_BP_A = np.asarray(_ba, dtype=np.float32).astype(np.float64)
+_z, _p, _k = tf2zpk(_BP_B, _BP_A)
+# numerator is exactly g * (1 - z^-2)^5: place the zeros exactly at +-1
+_z = np.array([1.0] * 5 + [-1.0] * 5)
+_BP_SOS = zpk2sos(_z, _p, _BP_B[0])
+_PRE_B = np.asarray(T.PRE_B, dtype=np.float32).astype(np.float64)
+_PRE_A = np.asarray(T.PRE_A, dtype=np.float32).astype(np.float64)
+_TAPER = torch.arange(1, 16, dtype=torch.float64) / 16.0
+
+
+def pesq_frames(L: int) -> int:
+    Lp = L + (L % 256)
+    return 0 if Lp < 512 else 1 + (Lp - 512) // 256
+
+
+def pesq(clean: torch.Tensor, noisy: torch.Tensor) -> torch.Tensor:
+    """[B, L] 16 kHz float32 -> MOS [B] float64."""
+    B, L = clean.shape
+    F = pesq_frames(L)
+    if F < 20:
+        raise RuntimeError(f"maximum size for tensor at dimension 1 is {max(F, 0)} but size is 20")
+    x = torch.cat([clean, noisy], 0).to(torch.float64).numpy()
+    y = sosfilt(_BP_SOS, x, axis=1)
+    power = (y * y).sum(axis=1) / (L + 5120) / 1.04684
+    x = x * np.sqrt(1e7 / power)[:, None]
+    x[:, :15] *= _TAPER.numpy()
+    x[:, -15:] *= _TAPER.numpy()[::-1]
+    x = lfilter(_PRE_B, _PRE_A, x, axis=1)
+    pad = L % 256
+    xt = torch.from_numpy(x)
+    if pad:
+        xt = torch.nn.functional.pad(xt, (0, pad))
+    spec = torch.stft(xt, n_fft=512, hop_length=256, win_length=512, window=torch.hann_window(512, dtype=torch.float64),
+                      center=False, return_complex=True).abs().square().transpose(1, 2)    # [2B, F, 257]
+    spec[:, :, 0] = 0.0
+    bark = torch.einsum("ij,klj->kli", _FBANK, spec[:, :, :-1]) * _CORR
+    c, n = bark[:B], bark[B:]
+    silent = (c * (c > _THR * 100.0)).sum(2) < 1e7
+    keep = (~silent).unsqueeze(-1)
+    mc = (c * ((c > _THR * 100.0) & keep)).mean(1)
+    mn = (n * ((n > _THR * 100.0) & keep)).mean(1)
+    ratio = ((mn + 1000.0) / (mc + 1000.0)).clamp(0.01, 100.0)
+    ec = ratio.unsqueeze(1) * c
+    fr = ((ec * (ec > _THR)).sum(2) + 5e3) / ((n * (n > _THR)).sum(2) + 5e3)
+    fr2 = fr.clone()
+    fr2[:, 1:] = 0.8 * fr[:, 1:] + 0.2 * fr[:, :-1]
+    en = fr2.clamp(3e-4, 5.0).unsqueeze(-1) * n
+
+    def loud(p):
+        v = (2.0 * _THR) ** _EXP * ((0.5 + 0.5 * p / _THR) ** _EXP - 1.0)
+        return torch.where(p <= _THR, torch.zeros_like(v), v) * T.SL_16K
+
+    lc, ln = loud(ec), loud(en)
+    d = ln - lc
+    d = d.sign() * (d.abs() - 0.25 * torch.minimum(lc, ln)).clamp(min=0)
+    sym = (math.sqrt(_TW) * torch.sqrt(((_WB * d)[:, :, 1:] ** 2).sum(2))).clamp(min=1e-20)
+    a = ((en + 50.0) / (ec + 50.0)) ** 1.2
+    a = torch.where(a < 3.0, torch.zeros_like(a), a).clamp(max=12.0)
+    asym = (_WB * d * a)[:, :, 1:].abs().sum(2).clamp(min=1e-20)
+    w = (((ec * (ec > _THR)).sum(2) + 1e5) / 1e7) ** 0.04
+    sym = (sym / w).clamp(max=45.0)
+    asym = (asym / w).clamp(max=45.0)
+
+    def pool(v):
+        fr_ = v.unfold(1, 20, 10)
+        return (fr_ ** 6).mean(2).pow(1.0 / 6.0).square().mean(1).sqrt()
+
+    m = 4.5 - 0.1 * pool(sym) - 0.0309 * pool(asym)
+    return 0.999 + 4.0 / (1.0 + torch.exp(-1.3669 * m + 3.8224))
+
+
+# ----------------------------------------------------------------------------- STOI
+_SW = torch.hann_window(257)[1:].to(torch.float64)
+
+
+def _obm() -> torch.Tensor:
+    freqs = torch.linspace(0, 5000, 257, dtype=torch.float64)
+    k = torch.arange(15, dtype=torch.float64)
+    lo = 150 * torch.pow(2.0, (2 * k - 1) / 6)
+    hi = 150 * torch.pow(2.0, (2 * k + 1) / 6)
+    m = torch.zeros(15, 257, dtype=torch.float64)
+    for i in range(15):
+        m[i, int(torch.argmin((freqs - lo[i]).abs())):int(torch.argmin((freqs - hi[i]).abs()))] = 1
+    return m
+
+
+_OBM = _obm()
+_CLIP = 1 + 10 ** (15 / 20)
+
+
+def _norm(v: torch.Tensor, dim: int) -> torch.Tensor:
+    v = v - v.mean(dim=dim, keepdim=True)
+    n = v.norm(dim=dim, keepdim=True)
+    return torch.where(n > 0, v / torch.where(n > 0, n, torch.ones_like(n)), torch.zeros_like(v))
+
+
+def stoi(clean: torch.Tensor, noisy: torch.Tensor):
+    """[B, L10] 10 kHz -> (stoi [B], estoi [B]) float64; NaN where no 30-frame segment exists."""
+    B = clean.shape[0]
+    out_s = torch.full((B,), float("nan"), dtype=torch.float64)
+    out_e = torch.full((B,), float("nan"), dtype=torch.float64)
+    x = clean.to(torch.float64)
+    y = noisy.to(torch.float64)
+    if x.shape[1] < 256:
+        raise RuntimeError("STOI input shorter than one 256-sample frame at 10 kHz")
+    xf = x.unfold(1, 256, 128) * _SW
+    yf = y.unfold(1, 256, 128) * _SW
+    e = 20 * torch.log10(xf.norm(dim=2) + 1e-9)
+    keep = (e.amax(1, keepdim=True) - 40 - e) < 0
+    win512 = torch.zeros(512, dtype=torch.float64)
+    win512[128:384] = _SW
+    for b in range(B):
+        kx, ky = xf[b][keep[b]], yf[b][keep[b]]
+        n = kx.shape[0]
+        nseg = n - 31
+        if nseg <= 0:
+            continue
+        length = (n + 1) * 128
+        ox = torch.zeros(length, dtype=torch.float64)
+        oy = torch.zeros(length, dtype=torch.float64)
+        idx = (128 * torch.arange(n)[:, None] + torch.arange(256)[None, :]).reshape(-1)
+        ox.index_add_(0, idx, kx.reshape(-1))
+        oy.index_add_(0, idx, ky.reshape(-1))
+        sp = torch.stft(torch.stack([ox, oy]), n_fft=512, hop_length=128, win_length=512, window=win512,
+                        center=False, return_complex=True).abs().square()            # [2, 257, T]
+        tob = torch.sqrt(torch.matmul(_OBM, sp))                                      # [2, 15, T]
+        segs = tob.unfold(2, 30, 1)[:, :, :nseg]                                      # [2, 15, S, 30]
+        cx, cy = segs[0].transpose(0, 1), segs[1].transpose(0, 1)                     # [S, 15, 30]
+        alpha = cx.norm(dim=2, keepdim=True) / (cy.norm(dim=2, keepdim=True) + 1e-9)
+        yc = torch.minimum(cy * alpha, cx * _CLIP)
+        out_s[b] = (_norm(cx, 2) * _norm(yc, 2)).sum() / 15 / nseg
+        out_e[b] = (_norm(_norm(cx, 2), 1) * _norm(_norm(cy, 2), 1)).sum() / 30 / nseg
+    return out_s, out_e

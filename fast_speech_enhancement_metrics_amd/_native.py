@@ -1,0 +1,93 @@
+"""ctypes binding of libfsem.so (include/fsem.h), the gfx950 HIP engine.
+
+The library is loaded AFTER torch so that its ``libamdhip64.so.7`` dependency resolves to
+the HIP runtime torch already loaded (one runtime per process: torch's streams and device
+pointers are valid in the library).  There is no fallback: if the library is missing or
+cannot be loaded, every GPU entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("FSEM_LIB", os.path.join(_PKG, "lib", "libfsem.so"))
+
+FSEM_OK = 0
+FSEM_EINVAL = -1
+FSEM_EWORKSPACE = -2
+FSEM_ELAUNCH = -3
+FSEM_ESHORT = -4
+FSEM_ERATE = -5
+
+_lock = threading.Lock()
+_lib = None
+
+_c_i64 = ctypes.c_int64
+_c_i32 = ctypes.c_int32
+_c_sz = ctypes.c_size_t
+_vp = ctypes.c_void_p
+
+# name -> (restype, argtypes); every symbol include/fsem.h declares
+SIGNATURES = {
+    "fsem_strerror": (ctypes.c_char_p, [ctypes.c_int]),
+    "fsem_version": (ctypes.c_int, []),
+    "fsem_resample_length": (_c_i64, [_c_i64, _c_i32, _c_i32]),
+    "fsem_resample_f32": (ctypes.c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _c_i64, _c_i32, _c_i32, _vp]),
+    "fsem_pesq_workspace_bytes": (_c_sz, [_c_i64, _c_i64]),
+    "fsem_pesq_frames": (ctypes.c_int, [_c_i64]),
+    "fsem_pesq_wb_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_sz, _vp]),
+    "fsem_pesq_front_workspace_bytes": (_c_sz, [_c_i64, _c_i64]),
+    "fsem_pesq_front_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _c_sz, _vp]),
+    "fsem_pesq_back_workspace_bytes": (_c_sz, [_c_i64, _c_i64]),
+    "fsem_pesq_back_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _vp, _vp, _c_sz, _vp]),
+    "fsem_stoi_workspace_bytes": (_c_sz, [_c_i64, _c_i64, _c_i32]),
+    "fsem_stoi_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _c_i64, _c_i32, _vp, _vp, _vp, _c_sz, _vp]),
+    "fsem_stoi_tob_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_i64, _vp, _c_sz, _vp]),
+}
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def load() -> ctypes.CDLL:
+    """Load (once) and return the library; raises if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise ImportError(
+                    f"fsem HIP engine not built: {LIB_PATH} is missing "
+                    "(run `python -m fast_speech_enhancement_metrics_amd._build`)")
+            lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_LOCAL)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+    return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != FSEM_OK:
+        msg = load().fsem_strerror(rc).decode()
+        raise NativeError(f"{what}: {msg} ({rc})")
+
+
+def stream_handle(device: torch.device | None = None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t: torch.Tensor) -> int:
+    return t.data_ptr()
+
+
+def workspace(nbytes: int, device) -> torch.Tensor:
+    """Scratch from torch's caching allocator (cheap after the first call)."""
+    return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)

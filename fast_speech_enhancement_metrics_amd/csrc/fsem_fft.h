@@ -1,0 +1,84 @@
+// One-wave 512-point complex FFT (radix-8 Stockham) shared by the PESQ and STOI kernels.
+#pragma once
+#include "fsem_common.h"
+
+namespace fsem {
+#include "fsem_tables.inc"
+
+struct cf {
+  float r, i;
+};
+__device__ __forceinline__ cf cadd(cf a, cf b) { return {a.r + b.r, a.i + b.i}; }
+__device__ __forceinline__ cf csub(cf a, cf b) { return {a.r - b.r, a.i - b.i}; }
+__device__ __forceinline__ cf cmul(cf a, cf b) {
+  return {fmaf(a.r, b.r, -a.i * b.i), fmaf(a.r, b.i, a.i * b.r)};
+}
+__device__ __forceinline__ cf mul_mi(cf a) { return {a.i, -a.r}; }  // a * (-i)
+
+// In-register forward DFT of 8 points (radix-2 DIT, W8 = exp(-i pi/4)).
+__device__ __forceinline__ void dft8(cf v[8]) {
+  const float h = 0.70710678118654752f;
+  cf a0 = cadd(v[0], v[4]), a1 = csub(v[0], v[4]);
+  cf a2 = cadd(v[2], v[6]), a3 = mul_mi(csub(v[2], v[6]));
+  cf a4 = cadd(v[1], v[5]), a5 = csub(v[1], v[5]);
+  cf a6 = cadd(v[3], v[7]), a7 = mul_mi(csub(v[3], v[7]));
+  cf b0 = cadd(a0, a2), b2 = csub(a0, a2), b1 = cadd(a1, a3), b3 = csub(a1, a3);
+  cf c0 = cadd(a4, a6), c2 = csub(a4, a6), c1 = cadd(a5, a7), c3 = csub(a5, a7);
+  cf w1c1 = {h * (c1.r + c1.i), h * (c1.i - c1.r)};    // c1 * (1 - i)/sqrt2
+  cf w3c3 = {h * (c3.i - c3.r), -h * (c3.r + c3.i)};   // c3 * (-1 - i)/sqrt2
+  cf mic2 = mul_mi(c2);
+  v[0] = cadd(b0, c0);
+  v[4] = csub(b0, c0);
+  v[1] = cadd(b1, w1c1);
+  v[5] = csub(b1, w1c1);
+  v[2] = cadd(b2, mic2);
+  v[6] = csub(b2, mic2);
+  v[3] = cadd(b3, w3c3);
+  v[7] = csub(b3, w3c3);
+}
+
+// 512-point complex FFT of one wave, radix-8 Stockham, natural-order result in
+// v[r] = Z[lane + 64 r].  `buf` = this wave's 1024-float LDS exchange area.
+__device__ __forceinline__ void fft512_wave(cf v[8], float2 *buf, int lane, const cf tw1[8],
+                                            const cf tw2[8]) {
+  dft8(v);
+#pragma unroll
+  for (int r = 0; r < 8; ++r) buf[8 * lane + r] = make_float2(v[r].r, v[r].i);
+  wave_lds_fence();
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    float2 t = buf[lane + 64 * r];
+    v[r] = {t.x, t.y};
+  }
+#pragma unroll
+  for (int r = 1; r < 8; ++r) v[r] = cmul(v[r], tw1[r]);
+  dft8(v);
+  wave_lds_fence();
+  const int o1 = (lane >> 3) * 64 + (lane & 7);
+#pragma unroll
+  for (int r = 0; r < 8; ++r) buf[o1 + 8 * r] = make_float2(v[r].r, v[r].i);
+  wave_lds_fence();
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    float2 t = buf[lane + 64 * r];
+    v[r] = {t.x, t.y};
+  }
+#pragma unroll
+  for (int r = 1; r < 8; ++r) v[r] = cmul(v[r], tw2[r]);
+  dft8(v);
+  wave_lds_fence();
+}
+
+
+// Per-lane twiddles of stages 1 and 2: W512^(8 r (lane&7)) and W512^(r lane).
+__device__ __forceinline__ void fft512_twiddles(int lane, cf tw1[8], cf tw2[8]) {
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const int i1 = (8 * r * (lane & 7)) & 511;
+    const int i2 = (r * lane) & 511;
+    tw1[r] = {kTwRe[i1], kTwIm[i1]};
+    tw2[r] = {kTwRe[i2], kTwIm[i2]};
+  }
+}
+
+}  // namespace fsem

@@ -1,0 +1,447 @@
+// STOI / ESTOI engine for gfx950 (MI355X).
+//
+// Replaces the reference's STOI.compute_stoi / compute_metric
+// (fast_se_metrics/STOI.py:153-205) and, for 16 kHz (any non-10 kHz) input, the
+// BaseMetric resampler (base.py:19-20) -- the 16 -> 10 kHz polyphase resampling is fused
+// into the kernels that consume the 10 kHz signal, so the resampled signal never exists
+// in HBM.  Four kernels per call:
+//
+//  stoi_vad      per (utterance, 64 VAD frames): resample the clean signal on the fly,
+//                frame energies of hann(257)[1:]-windowed 256-sample frames, hop 128, in dB
+//                (STOI.py:92-99).  Energy of frame i = P[i] + Q[i+1] over 128-sample blocks.
+//  stoi_select   per utterance: 40 dB voice-activity selection against the loudest clean
+//                frame, stream compaction of the kept frame indices (STOI.py:101-108).
+//  stoi_tob      per (utterance, 32 STFT frames): overlap-added signal built directly from
+//                the kept frames (STOI.py:71-86, never materialised), 512-point FFT of
+//                clean + i*denoised (one wave per frame pair), 15 one-third-octave band
+//                envelopes (STOI.py:49-69, 121-125).
+//  stoi_seg      per utterance: 30-frame segments -- equalisation + clipping, row / column
+//                normalisation and correlations for STOI and ESTOI (STOI.py:113-198), one
+//                lane per segment, band envelopes staged in LDS (no 30x materialisation).
+#include "fsem_fft.h"
+#include "fsem_resample.h"
+
+namespace fsem {
+namespace stoi {
+
+constexpr int NB = 15;     // one-third octave bands
+constexpr int NSEG = 30;   // frames per segment
+constexpr int VF = 64;     // VAD frames per workgroup
+constexpr int TF = 32;     // STFT frames per workgroup
+constexpr float kClip = 1.0f + 5.62341325190349f;  // 1 + 10^(-beta/20), beta = -15 (STOI.py:136-137)
+
+struct Src {
+  const float *x;  // input row base (clean or denoised)
+  int64_t n;       // input length at the input rate
+};
+
+// 10 kHz sample o of a row: either the input itself (sr == 10 kHz) or the fused resampler.
+__device__ __forceinline__ float sample10(const Src &s, int64_t o, int64_t L10, bool direct,
+                                          const ResampleKernel &rk) {
+  if (o < 0 || o >= L10) return 0.f;
+  return direct ? s.x[o] : resample_at(s.x, s.n, o, rk);
+}
+
+__global__ void __launch_bounds__(256)
+    stoi_vad(const float *__restrict__ ref, int64_t n_in, int64_t ld, int64_t L10, int NV, bool direct,
+             ResampleKernel rk, float *__restrict__ energy, int nv_ld) {
+  __shared__ float P[VF + 1], Q[VF + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t b = blockIdx.y;
+  const int i0 = blockIdx.x * VF;
+  const Src src{ref + b * ld, n_in};
+  const float wa = kHann256s[lane], wb = kHann256s[lane + 64];
+  const float wc = kHann256s[lane + 128], wd = kHann256s[lane + 192];
+  for (int j = wave; j <= VF; j += 4) {
+    const int64_t q = i0 + j;  // block index
+    const float y0 = sample10(src, 128 * q + lane, L10, direct, rk);
+    const float y1 = sample10(src, 128 * q + 64 + lane, L10, direct, rk);
+    // P: first half of frame q (window w[0..127]); Q: second half of frame q-1 (w[128..255])
+    const float p = wave_sum((wa * y0) * (wa * y0) + (wb * y1) * (wb * y1));
+    const float qq = wave_sum((wc * y0) * (wc * y0) + (wd * y1) * (wd * y1));
+    if (lane == 0) {
+      P[j] = p;
+      Q[j] = qq;
+    }
+  }
+  __syncthreads();
+  if (tid < VF) {
+    const int i = i0 + tid;
+    if (i < NV) {
+      const float e = P[tid] + Q[tid + 1];
+      energy[b * nv_ld + i] = 20.f * log10f(sqrtf(e) + 1e-9f);  // STOI.py:99
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256)
+    stoi_select(const float *__restrict__ energy, int nv_ld, int NV, int *__restrict__ idx,
+                int *__restrict__ kept) {
+  __shared__ float red[8];
+  __shared__ int wcount[4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t b = blockIdx.x;
+  const float *e = energy + b * nv_ld;
+  float m = -INFINITY;
+  for (int i = tid; i < NV; i += 256) m = fmaxf(m, e[i]);
+  m = block_max_256(m, red);
+  const float thr = m - 40.f;  // (max - dynamic_range - e) < 0  (STOI.py:102)
+  int base = 0;
+  for (int i0 = 0; i0 < NV; i0 += 256) {
+    const int i = i0 + tid;
+    const bool keep = (i < NV) && ((thr - e[i]) < 0.f);
+    const unsigned long long bal = __ballot(keep);
+    const int pre = __popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) wcount[wave] = __popcll(bal);
+    __syncthreads();
+    int off = base;
+    for (int w = 0; w < wave; ++w) off += wcount[w];
+    if (keep) idx[b * nv_ld + off + pre] = i;
+    base += wcount[0] + wcount[1] + wcount[2] + wcount[3];
+    __syncthreads();
+  }
+  if (tid == 0) kept[b] = base;
+}
+
+__global__ void __launch_bounds__(256)
+    stoi_tob(const float *__restrict__ ref, const float *__restrict__ deg, int64_t B, int64_t n_in,
+             int64_t ld, int64_t L10, bool direct, ResampleKernel rk, const int *__restrict__ idx,
+             const int *__restrict__ kept, int nv_ld, float *__restrict__ tob, int64_t tmax) {
+  __shared__ __attribute__((aligned(16))) float blk[2][TF + 1][128];
+  __shared__ __attribute__((aligned(16))) float xbuf[4 * 1024];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t b = blockIdx.y;
+  const int n = kept[b];
+  const int T = n - 2;  // STFT frames of the overlap-added signal: 1 + ((n+1)*128 - 512)/128
+  const int k0 = blockIdx.x * TF;
+  if (k0 >= T) return;
+  const int kend = min(k0 + TF, T);
+  const int *kidx = idx + b * nv_ld;
+  const Src sc{ref + b * ld, n_in}, sd{deg + b * ld, n_in};
+  const float w_lo = kHann256s[lane], w_lo2 = kHann256s[lane + 64];
+  const float w_hi = kHann256s[128 + lane], w_hi2 = kHann256s[128 + 64 + lane];
+
+  // overlap-added blocks q = k0+1 .. kend+1:  block_q[t] = w[t] F_{i_q}[t] + w[128+t] F_{i_{q-1}}[128+t]
+  const int nblk = kend - k0 + 1;
+  for (int j = wave; j < nblk; j += 4) {
+    const int q = k0 + 1 + j;
+    const int iq = kidx[q], ip = kidx[q - 1];
+    const int64_t a0 = 128LL * iq, a1 = 128LL * ip + 128;
+    float c0, c1, d0, d1;
+    if (a0 == a1) {  // consecutive kept frames: the two halves are the same samples
+      const float xc0 = sample10(sc, a0 + lane, L10, direct, rk);
+      const float xc1 = sample10(sc, a0 + 64 + lane, L10, direct, rk);
+      const float xd0 = sample10(sd, a0 + lane, L10, direct, rk);
+      const float xd1 = sample10(sd, a0 + 64 + lane, L10, direct, rk);
+      c0 = w_lo * xc0 + w_hi * xc0;
+      c1 = w_lo2 * xc1 + w_hi2 * xc1;
+      d0 = w_lo * xd0 + w_hi * xd0;
+      d1 = w_lo2 * xd1 + w_hi2 * xd1;
+    } else {
+      c0 = w_lo * sample10(sc, a0 + lane, L10, direct, rk) + w_hi * sample10(sc, a1 + lane, L10, direct, rk);
+      c1 = w_lo2 * sample10(sc, a0 + 64 + lane, L10, direct, rk) +
+           w_hi2 * sample10(sc, a1 + 64 + lane, L10, direct, rk);
+      d0 = w_lo * sample10(sd, a0 + lane, L10, direct, rk) + w_hi * sample10(sd, a1 + lane, L10, direct, rk);
+      d1 = w_lo2 * sample10(sd, a0 + 64 + lane, L10, direct, rk) +
+           w_hi2 * sample10(sd, a1 + 64 + lane, L10, direct, rk);
+    }
+    blk[0][j][lane] = c0;
+    blk[0][j][lane + 64] = c1;
+    blk[1][j][lane] = d0;
+    blk[1][j][lane + 64] = d1;
+  }
+  __syncthreads();
+
+  cf tw1[8], tw2[8];
+  fft512_twiddles(lane, tw1, tw2);
+  const float win[4] = {w_lo, w_lo2, w_hi, w_hi2};  // STFT window on the 256 centred samples
+  float2 *wbuf = reinterpret_cast<float2 *>(xbuf) + wave * 512;
+  float *pbuf = reinterpret_cast<float *>(wbuf);
+  const int plane = (64 - lane) & 63;
+  for (int k = k0 + wave; k < kend; k += 4) {
+    const int j = k - k0;  // frame k = [block_{k+1}, block_{k+2}] * w
+    cf v[8];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int jj = j + (r >> 1), t = lane + 64 * (r & 1);
+      v[r] = {blk[0][jj][t] * win[r], blk[1][jj][t] * win[r]};
+    }
+#pragma unroll
+    for (int r = 4; r < 8; ++r) v[r] = {0.f, 0.f};
+    fft512_wave(v, wbuf, lane, tw1, tw2);
+    float pc[4], pd[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float mr = __shfl(v[7 - r].r, plane, 64);
+      float mi = __shfl(v[7 - r].i, plane, 64);
+      if (lane == 0) {
+        mr = v[(8 - r) & 7].r;
+        mi = v[(8 - r) & 7].i;
+      }
+      const float zr = v[r].r, zi = v[r].i;
+      pc[r] = 0.25f * ((zr + mr) * (zr + mr) + (zi - mi) * (zi - mi));
+      pd[r] = 0.25f * ((zi + mi) * (zi + mi) + (zr - mr) * (zr - mr));
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      pbuf[lane + 64 * r] = pc[r];
+      pbuf[256 + lane + 64 * r] = pd[r];
+    }
+    wave_lds_fence();
+    if (lane < 2 * NB) {
+      const int sig = lane / NB, band = lane - sig * NB;
+      const float *ps = pbuf + 256 * sig;
+      float acc = 0.f;
+      for (int bin = kObmEdge[band][0]; bin < kObmEdge[band][1]; ++bin) acc += ps[bin];
+      tob[((b + sig * B) * NB + band) * tmax + k] = sqrtf(acc);
+    }
+    wave_lds_fence();
+  }
+}
+
+// One lane per 30-frame segment m: x[j][t] = X[j][m + t], y likewise (STOI.py:121-198).
+// 128-lane workgroups; per-lane row statistics of the ESTOI time normalisation are parked
+// in LDS ([stat][band][lane], conflict-free) between the row pass and the column pass.
+constexpr int SEG_T = 128;
+__global__ void __launch_bounds__(SEG_T)
+    stoi_seg(const float *__restrict__ tob, int64_t B, int64_t tmax, const int *__restrict__ kept,
+             float *__restrict__ stoi_out, float *__restrict__ estoi_out) {
+  constexpr int W = SEG_T + NSEG;  // frames per pass
+  constexpr int LDX = W + 1;
+  __shared__ float X[NB][LDX], Y[NB][LDX];
+  __shared__ float stat[4][NB][SEG_T];  // mu_x, 1/|x - mu_x|, mu_y, 1/|y - mu_y|
+  __shared__ double red[4];
+  const int tid = threadIdx.x;
+  const int64_t b = blockIdx.x;
+  const int n = kept[b];
+  const int S = n - 31;  // num_segments = (len - 512)//128 - 30 + 2 with len = (n+1)*128 (STOI.py:183-186)
+  if (S <= 0) {
+    if (tid == 0) {
+      stoi_out[b] = __builtin_nanf("");
+      estoi_out[b] = __builtin_nanf("");
+    }
+    return;
+  }
+  const int T = n - 2;
+  const float *xc = tob + (b * NB) * tmax;
+  const float *xd = tob + ((b + B) * NB) * tmax;
+  double st = 0.0, et = 0.0;
+  for (int m0 = 0; m0 < S; m0 += SEG_T) {
+    __syncthreads();
+    const int nf = min(W, T - m0);
+    for (int e = tid; e < NB * W; e += SEG_T) {
+      const int j = e / W, t = e - j * W;
+      X[j][t] = (t < nf) ? xc[j * tmax + m0 + t] : 0.f;
+      Y[j][t] = (t < nf) ? xd[j * tmax + m0 + t] : 0.f;
+    }
+    __syncthreads();
+    const int m = m0 + tid;
+    if (m < S) {
+      float s_acc = 0.f;
+      for (int j = 0; j < NB; ++j) {
+        float x[NSEG], y[NSEG];
+        float sx2 = 0.f, sy2 = 0.f, sx = 0.f, sy = 0.f;
+#pragma unroll
+        for (int t = 0; t < NSEG; ++t) {
+          x[t] = X[j][tid + t];
+          y[t] = Y[j][tid + t];
+          sx2 = fmaf(x[t], x[t], sx2);
+          sy2 = fmaf(y[t], y[t], sy2);
+          sx += x[t];
+          sy += y[t];
+        }
+        // equalize_clip (STOI.py:129-139)
+        const float alpha = sqrtf(sx2) / (sqrtf(sy2) + 1e-9f);
+        float syc = 0.f;
+#pragma unroll
+        for (int t = 0; t < NSEG; ++t) syc += fminf(alpha * y[t], x[t] * kClip);
+        const float mx = sx / NSEG, my = sy / NSEG, myc = syc / NSEG;
+        float dxx = 0.f, dyy = 0.f, dcc = 0.f, dxc = 0.f;
+#pragma unroll
+        for (int t = 0; t < NSEG; ++t) {
+          const float dx = x[t] - mx, dy = y[t] - my;
+          const float dc = fminf(alpha * y[t], x[t] * kClip) - myc;
+          dxx = fmaf(dx, dx, dxx);
+          dyy = fmaf(dy, dy, dyy);
+          dcc = fmaf(dc, dc, dcc);
+          dxc = fmaf(dx, dc, dxc);
+        }
+        const float nx = sqrtf(dxx), ny = sqrtf(dyy), nc = sqrtf(dcc);
+        // normalize() (STOI.py:113-119); a zero-variance row normalises to 0 here
+        s_acc += (nx > 0.f && nc > 0.f) ? dxc / (nx * nc) : 0.f;
+        stat[0][j][tid] = mx;
+        stat[1][j][tid] = nx > 0.f ? 1.f / nx : 0.f;
+        stat[2][j][tid] = my;
+        stat[3][j][tid] = ny > 0.f ? 1.f / ny : 0.f;
+      }
+      // ESTOI: time-normalised rows, then band (column) normalisation (STOI.py:178-181)
+      float mux[NB], rx[NB], muy[NB], ry[NB];
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        mux[j] = stat[0][j][tid];
+        rx[j] = stat[1][j][tid];
+        muy[j] = stat[2][j][tid];
+        ry[j] = stat[3][j][tid];
+      }
+      float e_acc = 0.f;
+      for (int t = 0; t < NSEG; ++t) {
+        float a[NB], c[NB];
+        float ma = 0.f, mc = 0.f;
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          a[j] = (X[j][tid + t] - mux[j]) * rx[j];
+          c[j] = (Y[j][tid + t] - muy[j]) * ry[j];
+          ma += a[j];
+          mc += c[j];
+        }
+        ma /= NB;
+        mc /= NB;
+        float aa = 0.f, cc = 0.f, ac = 0.f;
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          const float da = a[j] - ma, dc = c[j] - mc;
+          aa = fmaf(da, da, aa);
+          cc = fmaf(dc, dc, cc);
+          ac = fmaf(da, dc, ac);
+        }
+        const float na = sqrtf(aa), nc = sqrtf(cc);
+        e_acc += (na > 0.f && nc > 0.f) ? ac / (na * nc) : 0.f;
+      }
+      st += (double)s_acc;
+      et += (double)e_acc;
+    }
+  }
+  // deterministic 2-wave reduction
+  st = wave_sum_d(st);
+  et = wave_sum_d(et);
+  __syncthreads();
+  if ((tid & 63) == 0) {
+    red[(tid >> 6) * 2] = st;
+    red[(tid >> 6) * 2 + 1] = et;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    stoi_out[b] = (float)((red[0] + red[2]) / NB / S);   // compute_correlation / num_segments (STOI.py:150,198)
+    estoi_out[b] = (float)((red[1] + red[3]) / NSEG / S);
+  }
+}
+
+struct Geometry {
+  int64_t L10;
+  int NV, nv_ld, tmax;
+  bool direct;
+};
+
+inline int make_geometry(int64_t length, int32_t sr, Geometry *g, ResampleKernel *rk) {
+  g->direct = (sr == 10000);
+  if (g->direct) {
+    g->L10 = length;
+    rk->orig = rk->nw = 1;
+    rk->taps = 1;
+    rk->width = 0;
+  } else {
+    const int rc = make_resample_kernel(sr, 10000, rk);
+    if (rc != FSEM_OK) return rc;
+    g->L10 = (rk->nw * length + rk->orig - 1) / rk->orig;
+  }
+  g->NV = g->L10 >= 256 ? (int)((g->L10 - 256) / 128 + 1) : 0;
+  g->nv_ld = (int)align_up((size_t)(g->NV > 0 ? g->NV : 1), 64);
+  g->tmax = g->NV > 2 ? g->NV - 2 : 1;
+  return FSEM_OK;
+}
+
+inline size_t ws_bytes(int64_t B, const Geometry &g) {
+  size_t s = 0;
+  s += align_up(sizeof(float) * (size_t)B * g.nv_ld, 256);                // energies
+  s += align_up(sizeof(int) * (size_t)B * g.nv_ld, 256);                  // kept indices
+  s += align_up(sizeof(int) * (size_t)B, 256);                            // kept counts
+  s += align_up(sizeof(float) * (size_t)(2 * B) * NB * (size_t)g.tmax, 256);  // tob
+  return s;
+}
+
+inline int run(const float *ref, const float *deg, int64_t B, int64_t length, int64_t ld, int32_t sr,
+               float *stoi_out, float *estoi_out, int32_t *kept_out, float *tob_out, int64_t tob_ld,
+               void *ws, size_t ws_size, hipStream_t st) {
+  Geometry g;
+  ResampleKernel rk;
+  int rc = make_geometry(length, sr, &g, &rk);
+  if (rc != FSEM_OK) return rc;
+  if (g.NV <= 0) return FSEM_ESHORT;
+  if (!ws || ws_size < ws_bytes(B, g)) return FSEM_EWORKSPACE;
+  if (B > 65535) return FSEM_EINVAL;
+  char *p = static_cast<char *>(ws);
+  float *energy = reinterpret_cast<float *>(p);
+  p += align_up(sizeof(float) * (size_t)B * g.nv_ld, 256);
+  int *idx = reinterpret_cast<int *>(p);
+  p += align_up(sizeof(int) * (size_t)B * g.nv_ld, 256);
+  int *kept = reinterpret_cast<int *>(p);
+  p += align_up(sizeof(int) * (size_t)B, 256);
+  float *tob = reinterpret_cast<float *>(p);
+  int64_t tmax = g.tmax;
+  if (tob_out) {
+    tob = tob_out;
+    tmax = tob_ld;
+  }
+  if (kept_out) kept = kept_out;
+  hipLaunchKernelGGL(stoi_vad, dim3((unsigned)((g.NV + VF - 1) / VF), (unsigned)B), dim3(256), 0, st, ref,
+                     length, ld, g.L10, g.NV, g.direct, rk, energy, g.nv_ld);
+  FSEM_CHECK_LAUNCH();
+  hipLaunchKernelGGL(stoi_select, dim3((unsigned)B), dim3(256), 0, st, energy, g.nv_ld, g.NV, idx, kept);
+  FSEM_CHECK_LAUNCH();
+  hipLaunchKernelGGL(stoi_tob, dim3((unsigned)((g.tmax + TF - 1) / TF), (unsigned)B), dim3(256), 0, st, ref,
+                     deg, B, length, ld, g.L10, g.direct, rk, idx, kept, g.nv_ld, tob, tmax);
+  FSEM_CHECK_LAUNCH();
+  if (stoi_out) {
+    hipLaunchKernelGGL(stoi_seg, dim3((unsigned)B), dim3(SEG_T), 0, st, tob, B, tmax, kept, stoi_out,
+                       estoi_out);
+    FSEM_CHECK_LAUNCH();
+  }
+  return FSEM_OK;
+}
+
+}  // namespace stoi
+}  // namespace fsem
+
+using namespace fsem;
+
+extern "C" size_t fsem_stoi_workspace_bytes(int64_t batch, int64_t length, int32_t sample_rate) {
+  stoi::Geometry g;
+  ResampleKernel rk;
+  if (stoi::make_geometry(length, sample_rate, &g, &rk) != FSEM_OK) return 0;
+  return stoi::ws_bytes(batch, g);
+}
+
+extern "C" int fsem_stoi_f32(const float *ref, const float *deg, int64_t batch, int64_t length, int64_t ld,
+                             int32_t sample_rate, float *stoi_out, float *estoi_out, void *ws, size_t ws_bytes,
+                             void *stream) {
+  if (!ref || !deg || !stoi_out || !estoi_out || batch <= 0 || length <= 0 || ld < length) return FSEM_EINVAL;
+  return stoi::run(ref, deg, batch, length, ld, sample_rate, stoi_out, estoi_out, nullptr, nullptr, 0, ws,
+                   ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" int fsem_stoi_tob_f32(const float *ref10, const float *deg10, int64_t batch, int64_t length10,
+                                 int64_t ld, int32_t *kept, float *tob, int64_t tmax, void *ws, size_t ws_bytes,
+                                 void *stream) {
+  if (!ref10 || !deg10 || !kept || !tob || batch <= 0 || length10 <= 0 || ld < length10) return FSEM_EINVAL;
+  stoi::Geometry g;
+  ResampleKernel rk;
+  int rc = stoi::make_geometry(length10, 10000, &g, &rk);
+  if (rc != FSEM_OK) return rc;
+  if (tmax < g.tmax) return FSEM_EINVAL;
+  return stoi::run(ref10, deg10, batch, length10, ld, 10000, nullptr, nullptr, kept, tob, tmax, ws, ws_bytes,
+                   (hipStream_t)stream);
+}
+
+extern "C" const char *fsem_strerror(int code) {
+  switch (code) {
+    case FSEM_OK: return "ok";
+    case FSEM_EINVAL: return "invalid argument";
+    case FSEM_EWORKSPACE: return "workspace too small";
+    case FSEM_ELAUNCH: return "HIP launch failed";
+    case FSEM_ESHORT: return "input too short for the metric";
+    case FSEM_ERATE: return "unsupported sample-rate pair";
+    default: return "unknown error";
+  }
+}
+
+extern "C" int fsem_version(void) { return 1; }

@@ -1,0 +1,106 @@
+/*
+ * fsem.h -- C-ABI of libfsem.so, the MI355X (gfx950) engine behind
+ * fast_speech_enhancement_metrics_amd.PESQ / .STOI.
+ *
+ * The reference (kcoost/fast_speech_enhancement_metrics) is a pure-Python/PyTorch
+ * library with no FFI layer; its drop-in boundary is the metric class API
+ *   BaseMetric.__call__(clean, denoised) -> list[dict]      fast_se_metrics/base.py:41-43
+ * Each entry point below replaces the reference computation named next to it; the
+ * Python host layer (fast_speech_enhancement_metrics_amd/base.py, PESQ.py, STOI.py) keeps
+ * the reference's class API and calls these through ctypes.
+ *
+ * Conventions
+ *  - every pointer argument is DEVICE memory owned by the caller (torch tensors);
+ *  - the library allocates nothing: scratch space comes from `ws` (size from the
+ *    matching *_workspace_bytes query); work is enqueued asynchronously on `stream`
+ *    (a hipStream_t; NULL = the default stream) and the call returns immediately;
+ *  - signals are float32 rows: element (b, t) of a batch lives at ptr[b * ld + t];
+ *  - return 0 on success or a negative FSEM_E* code (fsem_strerror() for text);
+ *  - re-entrant across streams / devices (launches use the current HIP device).
+ */
+#ifndef FSEM_H
+#define FSEM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FSEM_OK 0
+#define FSEM_EINVAL -1        /* bad argument (sizes, null pointers)               */
+#define FSEM_EWORKSPACE -2    /* workspace smaller than *_workspace_bytes()        */
+#define FSEM_ELAUNCH -3       /* HIP launch / runtime error                        */
+#define FSEM_ESHORT -4        /* input too short for the metric (see each entry)  */
+#define FSEM_ERATE -5         /* unsupported sample-rate pair                      */
+
+const char *fsem_strerror(int code);
+int fsem_version(void);
+
+/* ---------------------------------------------------------------- resampling
+ * torchaudio.transforms.Resample(orig, new) (sinc_interp_hann, width 6,
+ * rolloff 0.99) as used by BaseMetric.prepare_audio   fast_se_metrics/base.py:13,19-20
+ * out: [rows, fsem_resample_length(n_in, orig, new)] with row stride ld_out.
+ */
+int64_t fsem_resample_length(int64_t n_in, int32_t orig_freq, int32_t new_freq);
+int fsem_resample_f32(const float *in, int64_t rows, int64_t n_in, int64_t ld_in,
+                      float *out, int64_t ld_out, int32_t orig_freq, int32_t new_freq,
+                      void *stream);
+
+/* ---------------------------------------------------------------- PESQ-wb
+ * Whole-metric entry: replaces PESQ.compute_metric    fast_se_metrics/PESQ.py:232-245
+ * (get_disturbances :174-230 + MOS mapping :240-243) for 16 kHz input.
+ *   ref, deg : [batch, length] float32 (row stride ld)  -- clean / denoised
+ *   mos      : [batch] float32 output
+ * FSEM_ESHORT when the padded length yields < 20 frames (the reference's
+ * unfold(1, 20, 10) raises RuntimeError there, PESQ.py:169).
+ */
+size_t fsem_pesq_workspace_bytes(int64_t batch, int64_t length);
+int fsem_pesq_frames(int64_t length);  /* F = 1 + (L + L%256 - 512) / 256 (PESQ.py:128-133) */
+int fsem_pesq_wb_f32(const float *ref, const float *deg, int64_t batch, int64_t length,
+                     int64_t ld, float *mos, void *ws, size_t ws_bytes, void *stream);
+
+/* Stage entries (same math, split for parity tests of intermediates):
+ * front: replaces PESQ.align_level's filtered power (PESQ.py:92-98) and
+ *        PESQ.get_bark_bands (PESQ.py:123-140) up to BarkFilterBank.forward
+ *        (bark.py:203-204), BEFORE the level scale:
+ *          bark  [2*batch, F, 49] float32 (rows 0..B-1 ref, B..2B-1 deg), unscaled
+ *          power [2*batch] float32 = sum_t filtered^2 (not yet / (L+5120) / 1.04684)
+ * back:  replaces PESQ.py:142-245 on those tensors -> mos [batch].
+ */
+size_t fsem_pesq_front_workspace_bytes(int64_t batch, int64_t length);
+int fsem_pesq_front_f32(const float *ref, const float *deg, int64_t batch, int64_t length,
+                        int64_t ld, float *bark, float *power, void *ws, size_t ws_bytes,
+                        void *stream);
+size_t fsem_pesq_back_workspace_bytes(int64_t batch, int64_t length);
+int fsem_pesq_back_f32(const float *bark, const float *power, int64_t batch, int64_t length,
+                       float *mos, void *ws, size_t ws_bytes, void *stream);
+
+/* ---------------------------------------------------------------- STOI / ESTOI
+ * Whole-metric entry: replaces STOI.compute_stoi + compute_metric
+ *   fast_se_metrics/STOI.py:153-205 (after BaseMetric resampling to 10 kHz,
+ *   base.py:19-20, when sample_rate != 10000).
+ *   ref, deg    : [batch, length] float32 at `sample_rate` (row stride ld)
+ *   stoi, estoi : [batch] float32 outputs; NaN where no 30-frame segment exists
+ *                 (the reference warns there, STOI.py:163-165).
+ */
+size_t fsem_stoi_workspace_bytes(int64_t batch, int64_t length, int32_t sample_rate);
+int fsem_stoi_f32(const float *ref, const float *deg, int64_t batch, int64_t length,
+                  int64_t ld, int32_t sample_rate, float *stoi, float *estoi, void *ws,
+                  size_t ws_bytes, void *stream);
+
+/* Intermediates of the 10 kHz STOI pipeline for parity tests:
+ *   kept  [batch] int32   -- frames kept by remove_silent_frames (STOI.py:88-111)
+ *   tob   [2*batch, 15, tmax] float32 third-octave band envelopes (STOI.py:121-125),
+ *         rows 0..B-1 ref, B..2B-1 deg; frames >= kept-2 are left untouched.
+ * Input must already be at 10 kHz (length = 10 kHz samples).
+ */
+int fsem_stoi_tob_f32(const float *ref10, const float *deg10, int64_t batch,
+                      int64_t length10, int64_t ld, int32_t *kept, float *tob, int64_t tmax,
+                      void *ws, size_t ws_bytes, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FSEM_H */
