@@ -42,35 +42,76 @@ __device__ __forceinline__ float sample10(const Src &s, int64_t o, int64_t L10, 
   return direct ? s.x[o] : resample_at(s.x, s.n, o, rk);
 }
 
+// Resample both signals of an utterance to 10 kHz once (written to the workspace, read
+// back only for the kept frames by stoi_tob) and compute the clean frame energies of this
+// chunk of VF frames.  Mode 0: 16 -> 10 kHz polyphase with the compile-time torchaudio
+// kernel kRs16k10k (each lane: one 8-in / 5-out group, 28 LDS reads, 140 FMAs with
+// uniform coefficients); mode 1: input already at 10 kHz; mode 2: generic rate pair.
+constexpr int VF2 = 32;                 // VAD frames per workgroup
+constexpr int YT = VF2 * 128 + 128;     // 10 kHz samples staged per workgroup
+constexpr int XT = (YT / 5 + 2) * 8 + 28;  // 16 kHz samples staged (mode 0)
 __global__ void __launch_bounds__(256)
-    stoi_vad(const float *__restrict__ ref, int64_t n_in, int64_t ld, int64_t L10, int NV, bool direct,
-             ResampleKernel rk, float *__restrict__ energy, int nv_ld) {
-  __shared__ float P[VF + 1], Q[VF + 1];
+    stoi_resample_vad(const float *__restrict__ ref, const float *__restrict__ deg, int64_t n_in, int64_t ld,
+                      int64_t L10, int NV, int mode, ResampleKernel rk, float *__restrict__ y10, int64_t y_ld,
+                      float *__restrict__ energy, int nv_ld) {
+  __shared__ __attribute__((aligned(16))) float xin[XT];
+  __shared__ __attribute__((aligned(16))) float ytile[YT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t b = blockIdx.y;
-  const int i0 = blockIdx.x * VF;
-  const Src src{ref + b * ld, n_in};
-  const float wa = kHann256s[lane], wb = kHann256s[lane + 64];
-  const float wc = kHann256s[lane + 128], wd = kHann256s[lane + 192];
-  for (int j = wave; j <= VF; j += 4) {
-    const int64_t q = i0 + j;  // block index
-    const float y0 = sample10(src, 128 * q + lane, L10, direct, rk);
-    const float y1 = sample10(src, 128 * q + 64 + lane, L10, direct, rk);
-    // P: first half of frame q (window w[0..127]); Q: second half of frame q-1 (w[128..255])
-    const float p = wave_sum((wa * y0) * (wa * y0) + (wb * y1) * (wb * y1));
-    const float qq = wave_sum((wc * y0) * (wc * y0) + (wd * y1) * (wd * y1));
-    if (lane == 0) {
-      P[j] = p;
-      Q[j] = qq;
+  const int64_t o0 = (int64_t)blockIdx.x * (VF2 * 128);
+  const int64_t o_end = min(o0 + (int64_t)YT, L10);
+  const int ny = (int)(o_end - o0);
+  const int nw_own = (int)min((int64_t)(VF2 * 128), L10 - o0);
+  for (int sig = 0; sig < 2; ++sig) {
+    const float *__restrict__ x = (sig == 0 ? ref : deg) + b * ld;
+    if (mode == 0) {
+      const int64_t m0 = o0 / 5;
+      const int64_t m1 = (o_end + 4) / 5;
+      const int64_t i0 = 8 * m0 - 10;
+      const int nin = (int)(8 * (m1 - m0) + 20);
+      for (int k = tid; k < nin; k += 256) {
+        const int64_t i = i0 + k;
+        xin[k] = (i >= 0 && i < n_in) ? x[i] : 0.f;
+      }
+      __syncthreads();
+      for (int64_t m = m0 + tid; m < m1; m += 256) {
+        const float *xs = xin + 8 * (m - m0);
+        float v[28];
+#pragma unroll
+        for (int t = 0; t < 28; ++t) v[t] = xs[t];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+          float acc = 0.f;
+#pragma unroll
+          for (int t = 0; t < 28; ++t) acc = fmaf(kRs16k10k[j][t], v[t], acc);
+          const int64_t o = 5 * m + j;
+          if (o >= o0 && o < o_end) ytile[o - o0] = acc;
+        }
+      }
+    } else {
+      const Src src{x, n_in};
+      for (int k = tid; k < ny; k += 256) ytile[k] = sample10(src, o0 + k, L10, mode == 1, rk);
     }
-  }
-  __syncthreads();
-  if (tid < VF) {
-    const int i = i0 + tid;
-    if (i < NV) {
-      const float e = P[tid] + Q[tid + 1];
-      energy[b * nv_ld + i] = 20.f * log10f(sqrtf(e) + 1e-9f);  // STOI.py:99
+    __syncthreads();
+    float *__restrict__ yr = y10 + (b * 2 + sig) * y_ld + o0;
+    for (int k = tid; k < nw_own; k += 256) yr[k] = ytile[k];
+    if (sig == 0) {
+      // frame energies 20 log10(||w * frame|| + 1e-9) (STOI.py:92-99)
+      for (int f = wave; f < VF2; f += 4) {
+        const int i = blockIdx.x * VF2 + f;
+        if (i >= NV) break;
+        const float *fr = ytile + 128 * f;
+        float acc = 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = kHann256s[lane + 64 * r] * fr[lane + 64 * r];
+          acc = fmaf(v, v, acc);
+        }
+        acc = wave_sum(acc);
+        if (lane == 0) energy[b * nv_ld + i] = 20.f * log10f(sqrtf(acc) + 1e-9f);
+      }
     }
+    __syncthreads();
   }
 }
 
@@ -104,8 +145,7 @@ __global__ void __launch_bounds__(256)
 }
 
 __global__ void __launch_bounds__(256)
-    stoi_tob(const float *__restrict__ ref, const float *__restrict__ deg, int64_t B, int64_t n_in,
-             int64_t ld, int64_t L10, bool direct, ResampleKernel rk, const int *__restrict__ idx,
+    stoi_tob(const float *__restrict__ y10, int64_t y_ld, int64_t B, int64_t L10, const int *__restrict__ idx,
              const int *__restrict__ kept, int nv_ld, float *__restrict__ tob, int64_t tmax) {
   __shared__ __attribute__((aligned(16))) float blk[2][TF + 1][128];
   __shared__ __attribute__((aligned(16))) float xbuf[4 * 1024];
@@ -117,7 +157,9 @@ __global__ void __launch_bounds__(256)
   if (k0 >= T) return;
   const int kend = min(k0 + TF, T);
   const int *kidx = idx + b * nv_ld;
-  const Src sc{ref + b * ld, n_in}, sd{deg + b * ld, n_in};
+  const float *__restrict__ yc = y10 + (b * 2) * y_ld;
+  const float *__restrict__ yd = yc + y_ld;
+  auto at = [L10](const float *__restrict__ y, int64_t o) { return (o < L10) ? y[o] : 0.f; };
   const float w_lo = kHann256s[lane], w_lo2 = kHann256s[lane + 64];
   const float w_hi = kHann256s[128 + lane], w_hi2 = kHann256s[128 + 64 + lane];
 
@@ -129,21 +171,21 @@ __global__ void __launch_bounds__(256)
     const int64_t a0 = 128LL * iq, a1 = 128LL * ip + 128;
     float c0, c1, d0, d1;
     if (a0 == a1) {  // consecutive kept frames: the two halves are the same samples
-      const float xc0 = sample10(sc, a0 + lane, L10, direct, rk);
-      const float xc1 = sample10(sc, a0 + 64 + lane, L10, direct, rk);
-      const float xd0 = sample10(sd, a0 + lane, L10, direct, rk);
-      const float xd1 = sample10(sd, a0 + 64 + lane, L10, direct, rk);
+      const float xc0 = at(yc, a0 + lane);
+      const float xc1 = at(yc, a0 + 64 + lane);
+      const float xd0 = at(yd, a0 + lane);
+      const float xd1 = at(yd, a0 + 64 + lane);
       c0 = w_lo * xc0 + w_hi * xc0;
       c1 = w_lo2 * xc1 + w_hi2 * xc1;
       d0 = w_lo * xd0 + w_hi * xd0;
       d1 = w_lo2 * xd1 + w_hi2 * xd1;
     } else {
-      c0 = w_lo * sample10(sc, a0 + lane, L10, direct, rk) + w_hi * sample10(sc, a1 + lane, L10, direct, rk);
-      c1 = w_lo2 * sample10(sc, a0 + 64 + lane, L10, direct, rk) +
-           w_hi2 * sample10(sc, a1 + 64 + lane, L10, direct, rk);
-      d0 = w_lo * sample10(sd, a0 + lane, L10, direct, rk) + w_hi * sample10(sd, a1 + lane, L10, direct, rk);
-      d1 = w_lo2 * sample10(sd, a0 + 64 + lane, L10, direct, rk) +
-           w_hi2 * sample10(sd, a1 + 64 + lane, L10, direct, rk);
+      c0 = w_lo * at(yc, a0 + lane) + w_hi * at(yc, a1 + lane);
+      c1 = w_lo2 * at(yc, a0 + 64 + lane) +
+           w_hi2 * at(yc, a1 + 64 + lane);
+      d0 = w_lo * at(yd, a0 + lane) + w_hi * at(yd, a1 + lane);
+      d1 = w_lo2 * at(yd, a0 + 64 + lane) +
+           w_hi2 * at(yd, a1 + 64 + lane);
     }
     blk[0][j][lane] = c0;
     blk[0][j][lane + 64] = c1;
@@ -329,7 +371,9 @@ __global__ void __launch_bounds__(SEG_T)
 struct Geometry {
   int64_t L10;
   int NV, nv_ld, tmax;
+  int64_t y_ld;
   bool direct;
+  int mode;
 };
 
 inline int make_geometry(int64_t length, int32_t sr, Geometry *g, ResampleKernel *rk) {
@@ -347,6 +391,8 @@ inline int make_geometry(int64_t length, int32_t sr, Geometry *g, ResampleKernel
   g->NV = g->L10 >= 256 ? (int)((g->L10 - 256) / 128 + 1) : 0;
   g->nv_ld = (int)align_up((size_t)(g->NV > 0 ? g->NV : 1), 64);
   g->tmax = g->NV > 2 ? g->NV - 2 : 1;
+  g->y_ld = (int64_t)align_up((size_t)g->L10, 64);
+  g->mode = g->direct ? 1 : ((sr == 16000) ? 0 : 2);
   return FSEM_OK;
 }
 
@@ -356,6 +402,7 @@ inline size_t ws_bytes(int64_t B, const Geometry &g) {
   s += align_up(sizeof(int) * (size_t)B * g.nv_ld, 256);                  // kept indices
   s += align_up(sizeof(int) * (size_t)B, 256);                            // kept counts
   s += align_up(sizeof(float) * (size_t)(2 * B) * NB * (size_t)g.tmax, 256);  // tob
+  s += align_up(sizeof(float) * (size_t)(2 * B) * (size_t)g.y_ld, 256);      // 10 kHz signals
   return s;
 }
 
@@ -383,13 +430,15 @@ inline int run(const float *ref, const float *deg, int64_t B, int64_t length, in
     tmax = tob_ld;
   }
   if (kept_out) kept = kept_out;
-  hipLaunchKernelGGL(stoi_vad, dim3((unsigned)((g.NV + VF - 1) / VF), (unsigned)B), dim3(256), 0, st, ref,
-                     length, ld, g.L10, g.NV, g.direct, rk, energy, g.nv_ld);
+  float *y10 = reinterpret_cast<float *>(reinterpret_cast<char *>(ws) + ws_bytes(B, g) -
+                                         align_up(sizeof(float) * (size_t)(2 * B) * (size_t)g.y_ld, 256));
+  hipLaunchKernelGGL(stoi_resample_vad, dim3((unsigned)((g.L10 + VF2 * 128 - 1) / (VF2 * 128)), (unsigned)B),
+                     dim3(256), 0, st, ref, deg, length, ld, g.L10, g.NV, g.mode, rk, y10, g.y_ld, energy, g.nv_ld);
   FSEM_CHECK_LAUNCH();
   hipLaunchKernelGGL(stoi_select, dim3((unsigned)B), dim3(256), 0, st, energy, g.nv_ld, g.NV, idx, kept);
   FSEM_CHECK_LAUNCH();
-  hipLaunchKernelGGL(stoi_tob, dim3((unsigned)((g.tmax + TF - 1) / TF), (unsigned)B), dim3(256), 0, st, ref,
-                     deg, B, length, ld, g.L10, g.direct, rk, idx, kept, g.nv_ld, tob, tmax);
+  hipLaunchKernelGGL(stoi_tob, dim3((unsigned)((g.tmax + TF - 1) / TF), (unsigned)B), dim3(256), 0, st, y10,
+                     g.y_ld, B, g.L10, idx, kept, g.nv_ld, tob, tmax);
   FSEM_CHECK_LAUNCH();
   if (stoi_out) {
     hipLaunchKernelGGL(stoi_seg, dim3((unsigned)B), dim3(SEG_T), 0, st, tob, B, tmax, kept, stoi_out,
