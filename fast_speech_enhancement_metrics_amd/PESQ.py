@@ -35,8 +35,11 @@ class PESQ(BaseMetric):
         if F < 20:
             # the reference's unfold(1, size=20, step=10) fails here (PESQ.py:169)
             raise RuntimeError(f"maximum size for tensor at dimension 1 is {max(F, 0)} but size is 20")
-        if clean.stride(0) != noisy.stride(0):
-            clean, noisy = clean.contiguous(), noisy.contiguous()
+        if clean.stride(0) != noisy.stride(0) or L % 4:
+            # rows must be readable up to ceil4(L) floats (include/fsem.h): pad odd lengths
+            pad = (-L) % 4
+            clean = torch.nn.functional.pad(clean, (0, pad)).contiguous()
+            noisy = torch.nn.functional.pad(noisy, (0, pad)).contiguous()
         mos = torch.empty(B, dtype=torch.float32, device=clean.device)
         ws = _native.workspace(lib.fsem_pesq_workspace_bytes(B, L), clean.device)
         _native.check(lib.fsem_pesq_wb_f32(clean.data_ptr(), noisy.data_ptr(), B, L, clean.stride(0),

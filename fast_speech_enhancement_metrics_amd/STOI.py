@@ -44,8 +44,11 @@ class STOI(BaseMetric):
                 clean, noisy = self.resampler(clean), self.resampler(noisy)
             return _cpu.stoi(clean, noisy)
         lib = _native.load()
-        if clean.stride(0) != noisy.stride(0):
-            clean, noisy = clean.contiguous(), noisy.contiguous()
+        if clean.stride(0) != noisy.stride(0) or L % 4:
+            # rows must be readable up to ceil4(L) floats (include/fsem.h): pad odd lengths
+            pad = (-L) % 4
+            clean = torch.nn.functional.pad(clean, (0, pad)).contiguous()
+            noisy = torch.nn.functional.pad(noisy, (0, pad)).contiguous()
         s = torch.empty(B, dtype=torch.float32, device=clean.device)
         e = torch.empty(B, dtype=torch.float32, device=clean.device)
         nbytes = lib.fsem_stoi_workspace_bytes(B, L, sr)

@@ -37,17 +37,22 @@ __device__ __forceinline__ void dft8(cf v[8]) {
   v[7] = csub(b3, w3c3);
 }
 
+// LDS exchange area per wave, in float2: 512 + 64 pad (index i stored at i + i/8, which
+// makes the stage-0/1 scatters and the strided gathers bank-conflict-free).
+constexpr int kFftBuf = 576;
+__device__ __forceinline__ int fpad(int i) { return i + (i >> 3); }
+
 // 512-point complex FFT of one wave, radix-8 Stockham, natural-order result in
-// v[r] = Z[lane + 64 r].  `buf` = this wave's 1024-float LDS exchange area.
+// v[r] = Z[lane + 64 r].  `buf` = this wave's kFftBuf-float2 LDS exchange area.
 __device__ __forceinline__ void fft512_wave(cf v[8], float2 *buf, int lane, const cf tw1[8],
                                             const cf tw2[8]) {
   dft8(v);
 #pragma unroll
-  for (int r = 0; r < 8; ++r) buf[8 * lane + r] = make_float2(v[r].r, v[r].i);
+  for (int r = 0; r < 8; ++r) buf[fpad(8 * lane + r)] = make_float2(v[r].r, v[r].i);
   wave_lds_fence();
 #pragma unroll
   for (int r = 0; r < 8; ++r) {
-    float2 t = buf[lane + 64 * r];
+    float2 t = buf[fpad(lane + 64 * r)];
     v[r] = {t.x, t.y};
   }
 #pragma unroll
@@ -56,11 +61,11 @@ __device__ __forceinline__ void fft512_wave(cf v[8], float2 *buf, int lane, cons
   wave_lds_fence();
   const int o1 = (lane >> 3) * 64 + (lane & 7);
 #pragma unroll
-  for (int r = 0; r < 8; ++r) buf[o1 + 8 * r] = make_float2(v[r].r, v[r].i);
+  for (int r = 0; r < 8; ++r) buf[fpad(o1 + 8 * r)] = make_float2(v[r].r, v[r].i);
   wave_lds_fence();
 #pragma unroll
   for (int r = 0; r < 8; ++r) {
-    float2 t = buf[lane + 64 * r];
+    float2 t = buf[fpad(lane + 64 * r)];
     v[r] = {t.x, t.y};
   }
 #pragma unroll

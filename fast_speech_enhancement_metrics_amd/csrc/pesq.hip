@@ -29,11 +29,27 @@
 // pesq_back   one 256-thread workgroup per utterance: level scale, silent frames, band and
 //   frame equalisation, Zwicker loudness, symmetric / asymmetric disturbance, L6/L2 pooling
 //   and the MOS mapping (PESQ.py:142-245), deterministic block reductions.
+#include <algorithm>
+
 #include "fsem_fft.h"
 
 namespace fsem {
 
 namespace pesq {
+
+#ifdef FSEM_STAMPS
+// Diagnostic build only (tools/stamps.py): s_memtime at phase boundaries of pesq_front.
+constexpr int kStampBlocks = 65536;
+__device__ unsigned long long g_stamps[kStampBlocks][16];
+#define STAMP(i)                                                                                   \
+  do {                                                                                             \
+    if (threadIdx.x == 0 && blockIdx.x < kStampBlocks) g_stamps[blockIdx.x][i] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define STAMP(i) \
+  do {           \
+  } while (0)
+#endif
 
 constexpr int PT = 256;
 constexpr int CH = FSEM_PESQ_CH;  // 60 samples per lane
@@ -42,294 +58,353 @@ constexpr int WARM = 768;
 constexpr int NF = 56;            // frames per segment
 constexpr int OWN = NF * 256;     // samples of band-pass power owned per segment
 constexpr int NBARK = 49;
-constexpr int SCAN_LD = 11;       // floats per lane in the scan buffer
-constexpr int XBUF = 4 * 1024;    // 4 waves x 512 complex
+constexpr int NS = 12;            // scan states: 10 band-pass (5 sections) + 2 pre-emphasis
+constexpr int SCAN_LD = 13;       // floats per lane in the scan buffer (odd: conflict-free)
+constexpr int XBUF = 4 * 2 * kFftBuf;  // 4 waves x 576 complex
 constexpr int SPEC_LD = 257;      // parked spectrum row stride (bank-conflict pad)
-constexpr int NBP = 10;           // band-pass states (5 sections)
+constexpr int NBP = 10;           // band-pass states
+constexpr int PF = TILE / 4 / PT; // float4 per thread per tile (prefetch registers)
 static_assert(WARM + 256 * (NF + 1) == TILE, "tile geometry");
 static_assert(PT * SCAN_LD <= XBUF, "scan buffer fits the exchange buffer");
-static_assert(SPEC_LD * 63 + 256 <= TILE + XBUF, "parked spectra stay in LDS");
+static_assert(SPEC_LD * (NF - 1) + 256 <= TILE, "parked spectra stay in the tile");
+static_assert(TILE % (4 * PT) == 0, "prefetch split");
 
+// PESQ.py:90,108-109: first 15 samples x (t+1)/16, last 15 samples x (L-t)/16, else 1:
+// w(t) = sat((t+1)/16) * sat((L-t)/16), exact in float32 for t, L < 2^24.
+__device__ __forceinline__ float taper_w(float tf, float Lf) {
+  return __saturatef((tf + 1.f) * 0.0625f) * __saturatef((Lf - tf) * 0.0625f);
+}
+
+struct Item {
+  int64_t s;       // signal (0..B-1 ref, B..2B-1 deg)
+  int g;           // segment
+  int64_t tstart;  // global sample index of tile[0]
+  const float *xrow;
+};
+
+__device__ __forceinline__ Item make_item(int64_t item, int nseg, int64_t B, int64_t ld,
+                                          const float *ref, const float *deg) {
+  Item it;
+  it.s = item / nseg;
+  it.g = (int)(item - it.s * nseg);
+  it.tstart = (int64_t)it.g * OWN - WARM;
+  it.xrow = (it.s < B) ? ref + it.s * ld : deg + (it.s - B) * ld;
+  return it;
+}
+
+// Issue the global loads of one tile into registers (consumed one item later).  Raw buffer
+// loads with a wave-uniform descriptor over [0, ceil4(L)): out-of-range float4s (t < 0 wraps
+// the 32-bit offset; t >= ceil4(L)) return zeros from the hardware range check.  Samples in
+// [L, ceil4(L)) may hold anything: both filters are causal and every output at t >= L is
+// masked, so they cannot reach a result (rows must be readable up to ceil4(L), include/fsem.h).
+__device__ __forceinline__ void prefetch(const Item &it, int64_t L, int tid, float4 pre[PF]) {
+  const uint64_t base = reinterpret_cast<uint64_t>(it.xrow);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
+  const uint32_t nbytes = __builtin_amdgcn_readfirstlane((uint32_t)(((L + 3) & ~(int64_t)3) * 4));
+  void *p = reinterpret_cast<void *>(((uint64_t)hi << 32) | lo);
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(p, 0, nbytes, 0x00020000);
+  const int t0 = (int)it.tstart;
+#pragma unroll
+  for (int k = 0; k < PF; ++k) {
+    const int t = t0 + 4 * (tid + PT * k);
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    const v4f v = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(rsrc, t * 4, 0, 0));
+    pre[k] = make_float4(v.x, v.y, v.z, v.w);
+  }
+}
+
+// IIR pass 1: end states of this lane's chunk from zero state -- band-pass (states 0..9,
+// untapered input) and pre-emphasis (states 10..11, tapered input).  Fully unrolled: the
+// kBpG / kPreG functionals become literal-operand FMAs.
+template <bool TAPER>
+__device__ __forceinline__ void iir_pass1(const float4 *__restrict__ my4, int64_t t_lane, int64_t L, float e[NS]) {
+  const float tf0 = (float)t_lane, Lf = (float)L;
+#pragma unroll
+  for (int i = 0; i < NS; ++i) e[i] = 0.f;
+#pragma unroll
+  for (int q = 0; q < CH / 4; ++q) {
+    const float4 v = my4[q];
+    const float xs[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int n = 4 * q + c;
+#pragma unroll
+      for (int i = 0; i < NBP; ++i) e[i] = fmaf(kBpG[n][i], xs[c], e[i]);
+      const float xp = TAPER ? xs[c] * taper_w(tf0 + (float)n, Lf) : xs[c];
+      e[NBP] = fmaf(kPreG[n][0], xp, e[NBP]);
+      e[NBP + 1] = fmaf(kPreG[n][1], xp, e[NBP + 1]);
+    }
+  }
+}
+
+// IIR pass 2 from the true start state z: band-pass cascade (power over owned samples) and
+// pre-emphasis, whose output overwrites the chunk in place (zero from `lim` on).
+template <bool TAPER>
+__device__ __forceinline__ float iir_pass2(float4 *__restrict__ w4, float z[NS], int own_lo, int own_hi,
+                                           int lim, int64_t t_lane, int64_t L) {
+  const float b0 = kPreB[0], b1 = kPreB[1], b2 = kPreB[2], a1 = kPreA[1], a2 = kPreA[2];
+  const float tf0 = (float)t_lane, Lf = (float)L;
+  float acc = 0.f;
+#pragma unroll 3
+  for (int q = 0; q < CH / 4; ++q) {
+    const float4 v = w4[q];
+    float xs[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int n = 4 * q + c;
+      float u = xs[c];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        const float y = u + z[2 * k];
+        z[2 * k] = fmaf(-kBpSecA[k][0], y, z[2 * k + 1]);
+        z[2 * k + 1] = fmaf(-kBpSecA[k][1], y, -u);
+        u = y;
+      }
+      acc = (n >= own_lo && n < own_hi) ? fmaf(u, u, acc) : acc;
+      const float xp = TAPER ? xs[c] * taper_w(tf0 + (float)n, Lf) : xs[c];
+      const float y = fmaf(b0, xp, z[NBP]);
+      z[NBP] = fmaf(b1, xp, fmaf(-a1, y, z[NBP + 1]));
+      z[NBP + 1] = fmaf(b2, xp, -a2 * y);
+      xs[c] = (n < lim) ? y : 0.f;  // the reference zero-pads AFTER the filter (PESQ.py:128)
+    }
+    w4[q] = make_float4(xs[0], xs[1], xs[2], xs[3]);
+  }
+  return acc;
+}
+
+// Persistent: each workgroup walks items (signal, segment) = blockIdx.x, +gridDim.x, ...;
+// the next item's tile is in flight in registers while the current one is processed.
 __global__ void __launch_bounds__(PT, 2)
     pesq_front(const float *__restrict__ ref, const float *__restrict__ deg, int64_t B, int64_t L,
-               int64_t ld, int F, int nseg, int npseg, float *__restrict__ bark,
+               int64_t ld, int F, int nseg, int npseg, int64_t nitems, float *__restrict__ bark,
                float *__restrict__ ppart) {
   __shared__ __attribute__((aligned(16))) float tile[TILE];
   __shared__ __attribute__((aligned(16))) float xbuf[XBUF];
   __shared__ float red[8];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t s = blockIdx.x / nseg;
-  const int g = (int)(blockIdx.x - s * nseg);
-  const float *__restrict__ xrow = (s < B) ? ref + s * ld : deg + (s - B) * ld;
-  const int64_t tstart = (int64_t)g * OWN - WARM;  // global sample index of tile[0]
-
-  // ---------------------------------------------------------------- A: load tile
-  {
-    const bool al = ((reinterpret_cast<uintptr_t>(xrow) & 15) == 0);
-    float4 *t4 = reinterpret_cast<float4 *>(tile);
-    for (int v = tid; v < TILE / 4; v += PT) {
-      const int64_t t = tstart + 4 * v;
-      float4 val;
-      if (al && t >= 0 && t + 3 < L) {
-        val = *reinterpret_cast<const float4 *>(xrow + t);
-      } else {
-        val.x = (t >= 0 && t < L) ? xrow[t] : 0.f;
-        val.y = (t + 1 >= 0 && t + 1 < L) ? xrow[t + 1] : 0.f;
-        val.z = (t + 2 >= 0 && t + 2 < L) ? xrow[t + 2] : 0.f;
-        val.w = (t + 3 >= 0 && t + 3 < L) ? xrow[t + 3] : 0.f;
-      }
-      t4[v] = val;
-    }
+  // ---- per-lane constants, loaded once
+  float win[8];
+  cf tw1[8], tw2[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) win[r] = kHann512[lane + 64 * r];
+  fft512_twiddles(lane, tw1, tw2);
+  const int plane = (64 - lane) & 63;
+  // Bark MFMA (v_mfma_f32_16x16x4_f32): wave w owns frame rows 16w..16w+15 of the segment and
+  // all four 16-band tiles; B operand = fbank x correction from per-lane band edges.
+  int blo_c[4], bhi_c[4];
+  float bcor_c[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int band = 16 * t + (lane & 15);
+    blo_c[t] = band < NBARK ? kBandEdge[band] : 0;
+    bhi_c[t] = band < NBARK ? kBandEdge[band + 1] : 0;
+    bcor_c[t] = band < NBARK ? kBarkCorr[band] : 0.f;
   }
-  __syncthreads();
 
-  const float4 *__restrict__ my4 = reinterpret_cast<const float4 *>(tile + CH * tid);
+  float4 pre[PF];
+  int64_t item = blockIdx.x;
+  if (item < nitems) prefetch(make_item(item, nseg, B, ld, ref, deg), L, tid, pre);
 
-  // ---------------------------------------------------------------- B: band-pass power
-  {
-    float e[NBP];
+  for (; item < nitems; item += gridDim.x) {
+    const Item it = make_item(item, nseg, B, ld, ref, deg);
+    STAMP(0);
+    {
+      float4 *t4 = reinterpret_cast<float4 *>(tile);
 #pragma unroll
-    for (int i = 0; i < NBP; ++i) e[i] = 0.f;
-#pragma unroll
-    for (int q = 0; q < CH / 4; ++q) {
-      const float4 v = my4[q];
-      const float xs[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-#pragma unroll
-        for (int i = 0; i < NBP; ++i) e[i] = fmaf(kBpG[4 * q + c][i], xs[c], e[i]);
-      }
+      for (int k = 0; k < PF; ++k) t4[tid + PT * k] = pre[k];
     }
-    // Hillis-Steele scan over the 256 chunks (truncated: state decays below 1e-14 in 16)
+    __syncthreads();
+    STAMP(1);
+    const int g = it.g;
+    const int64_t tstart = it.tstart;
+    const float4 *__restrict__ my4 = reinterpret_cast<const float4 *>(tile + CH * tid);
+    const int64_t t_lane = tstart + CH * tid;  // global index of this lane's first sample
+    // lanes whose chunk meets the tapered edges (PESQ.py:108-109); wave-uniform fast path
+    const bool edge = (t_lane < 15) || (t_lane + CH > L - 15 && t_lane < L);
+    const bool wave_edge = __any(edge);
+
+    // ---------------------------------------------------------------- IIR pass 1: end states
+    // band-pass (untapered input, PESQ.py:94) and pre-emphasis (tapered, PESQ.py:108-111)
+    float e[NS];
+    if (__builtin_amdgcn_readfirstlane((int)wave_edge))
+      iir_pass1<true>(my4, t_lane, L, e);
+    else
+      iir_pass1<false>(my4, t_lane, L, e);
+    STAMP(2);
+    // ---------------------------------------------------------------- chunk scan (4 levels)
+    float *const mine = xbuf + tid * SCAN_LD;
 #pragma unroll
-    for (int i = 0; i < NBP; ++i) xbuf[tid * SCAN_LD + i] = e[i];
+    for (int i = 0; i < NS; ++i) mine[i] = e[i];
     __syncthreads();
 #pragma unroll
     for (int lv = 0; lv < 4; ++lv) {
       const int d = 1 << lv;
-      float q[NBP];
+      float q[NS];
+      const float *src = xbuf + max(tid - d, 0) * SCAN_LD;  // one base + immediate offsets
+      const float keep = (tid >= d) ? 1.f : 0.f;
 #pragma unroll
-      for (int i = 0; i < NBP; ++i) q[i] = (tid >= d) ? xbuf[(tid - d) * SCAN_LD + i] : 0.f;
+      for (int i = 0; i < NS; ++i) q[i] = src[i] * keep;
       __syncthreads();
 #pragma unroll
       for (int i = 0; i < NBP; ++i) {
         float acc = e[i];
+        // the cascade's transition is block lower-triangular: section i/2 sees sections <= i/2
 #pragma unroll
-        for (int k = 0; k < NBP; ++k) acc = fmaf(kBpScan[lv][i][k], q[k], acc);
+        for (int k = 0; k < 2 * (i / 2) + 2; ++k) acc = fmaf(kBpScan[lv][i][k], q[k], acc);
         e[i] = acc;
       }
+      {
+        const float p0 = fmaf(kPreScan[lv][0][0], q[NBP], fmaf(kPreScan[lv][0][1], q[NBP + 1], e[NBP]));
+        const float p1 = fmaf(kPreScan[lv][1][0], q[NBP], fmaf(kPreScan[lv][1][1], q[NBP + 1], e[NBP + 1]));
+        e[NBP] = p0;
+        e[NBP + 1] = p1;
+      }
+      if (lv < 3) {
 #pragma unroll
-      for (int i = 0; i < NBP; ++i) xbuf[tid * SCAN_LD + i] = e[i];
-      __syncthreads();
-    }
-    float z[NBP];
-#pragma unroll
-    for (int i = 0; i < NBP; ++i) z[i] = (tid >= 1) ? xbuf[(tid - 1) * SCAN_LD + i] : 0.f;
-
-    // ownership window of this segment, in tile coordinates
-    const int64_t own_len64 = (g < npseg) ? ((L - (int64_t)g * OWN) < OWN ? (L - (int64_t)g * OWN) : OWN) : 0;
-    const int own_lo = WARM, own_hi = WARM + (int)own_len64;
-    float acc = 0.f;
-#pragma unroll 3
-    for (int q = 0; q < CH / 4; ++q) {
-      const float4 v = my4[q];
-      const float xs[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        float u = xs[c];
-#pragma unroll
-        for (int k = 0; k < 5; ++k) {
-          const float y = u + z[2 * k];
-          z[2 * k] = fmaf(-kBpSecA[k][0], y, z[2 * k + 1]);
-          z[2 * k + 1] = fmaf(-kBpSecA[k][1], y, -u);
-          u = y;
-        }
-        const int li = CH * tid + 4 * q + c;
-        acc = (li >= own_lo && li < own_hi) ? fmaf(u, u, acc) : acc;
+        for (int i = 0; i < NS; ++i) mine[i] = e[i];
+        __syncthreads();
       }
     }
-    const float tot = block_sum_256(acc, red);
-    if (tid == 0) ppart[s * nseg + g] = tot * (kBpGain * kBpGain);
+    // start state of chunk j = inclusive prefix of chunk j-1
+#pragma unroll
+    for (int i = 0; i < NS; ++i) mine[i] = e[i];
     __syncthreads();
-  }
-
-  // ---------------------------------------------------------------- C: taper (PESQ.py:108-109)
-  if (tid < 15) {
-    const int64_t t = tid;  // head: x[t] *= (t+1)/16
-    const int64_t li = t - tstart;
-    if (li >= 0 && li < TILE) tile[li] *= (float)(tid + 1) / 16.f;
-  } else if (tid >= 32 && tid < 47) {
-    const int64_t t = L - 15 + (tid - 32);  // tail: x[L-15+i] *= (15-i)/16
-    const int64_t li = t - tstart;
-    if (t >= 0 && li >= 0 && li < TILE) tile[li] *= (float)(15 - (tid - 32)) / 16.f;
-  }
-  __syncthreads();
-
-  // ---------------------------------------------------------------- D: pre-emphasis (PESQ.py:111)
-  {
-    float e0 = 0.f, e1 = 0.f;
+    float z[NS];
+    {
+      const float *src = xbuf + max(tid - 1, 0) * SCAN_LD;
+      const float keep = (tid >= 1) ? 1.f : 0.f;
 #pragma unroll
-    for (int q = 0; q < CH / 4; ++q) {
-      const float4 v = my4[q];
-      const float xs[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        e0 = fmaf(kPreG[4 * q + c][0], xs[c], e0);
-        e1 = fmaf(kPreG[4 * q + c][1], xs[c], e1);
-      }
+      for (int i = 0; i < NS; ++i) z[i] = src[i] * keep;
     }
-    xbuf[tid * SCAN_LD + 0] = e0;
-    xbuf[tid * SCAN_LD + 1] = e1;
+    STAMP(3);
+
+    // ---------------------------------------------------------------- IIR pass 2
+    {
+      const int64_t own_len = (g < npseg) ? min((int64_t)OWN, L - (int64_t)g * OWN) : 0;
+      const int own_lo = WARM - CH * tid, own_hi = WARM + (int)own_len - CH * tid;  // chunk-local
+      const int lim = (int)min((int64_t)CH, max((int64_t)0, L - t_lane));       // y = 0 from here
+      float4 *w4 = reinterpret_cast<float4 *>(tile + CH * tid);
+      float acc;
+      if (__builtin_amdgcn_readfirstlane((int)wave_edge))
+        acc = iir_pass2<true>(w4, z, own_lo, own_hi, lim, t_lane, L);
+      else
+        acc = iir_pass2<false>(w4, z, own_lo, own_hi, lim, t_lane, L);
+      const float tot = block_sum_256(acc, red);
+      if (tid == 0) ppart[it.s * nseg + g] = tot * (kBpGain * kBpGain);
+    }
     __syncthreads();
-#pragma unroll
-    for (int lv = 0; lv < 4; ++lv) {
-      const int d = 1 << lv;
-      const float q0 = (tid >= d) ? xbuf[(tid - d) * SCAN_LD + 0] : 0.f;
-      const float q1 = (tid >= d) ? xbuf[(tid - d) * SCAN_LD + 1] : 0.f;
-      __syncthreads();
-      e0 = fmaf(kPreScan[lv][0][0], q0, fmaf(kPreScan[lv][0][1], q1, e0));
-      e1 = fmaf(kPreScan[lv][1][0], q0, fmaf(kPreScan[lv][1][1], q1, e1));
-      xbuf[tid * SCAN_LD + 0] = e0;
-      xbuf[tid * SCAN_LD + 1] = e1;
-      __syncthreads();
+    STAMP(4);
+    // issue the next item's tile loads now: they stay in flight through the FFT / Bark
+    // phases (the IIR phases above run without the prefetch registers live)
+    {
+      const int64_t nxt = item + gridDim.x;
+      if (nxt < nitems) prefetch(make_item(nxt, nseg, B, ld, ref, deg), L, tid, pre);
     }
-    float z0 = (tid >= 1) ? xbuf[(tid - 1) * SCAN_LD + 0] : 0.f;
-    float z1 = (tid >= 1) ? xbuf[(tid - 1) * SCAN_LD + 1] : 0.f;
-    const float b0 = kPreB[0], b1 = kPreB[1], b2 = kPreB[2], a1 = kPreA[1], a2 = kPreA[2];
-    const int64_t lim = L - tstart;  // tile index of the first sample >= L
-    float4 *w4 = reinterpret_cast<float4 *>(tile + CH * tid);
-#pragma unroll 3
-    for (int q = 0; q < CH / 4; ++q) {
-      const float4 v = w4[q];
-      float xs[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const float u = xs[c];
-        const float y = fmaf(b0, u, z0);
-        z0 = fmaf(b1, u, fmaf(-a1, y, z1));
-        z1 = fmaf(b2, u, -a2 * y);
-        const int li = CH * tid + 4 * q + c;
-        xs[c] = (li < lim) ? y : 0.f;  // the reference zero-pads AFTER the filter (PESQ.py:128)
-      }
-      w4[q] = make_float4(xs[0], xs[1], xs[2], xs[3]);
-    }
-  }
-  __syncthreads();
 
-  // ---------------------------------------------------------------- E: FFT + Bark (MFMA)
-  const int nfr = min(NF, F - g * NF);  // valid frames in this segment
-  if (nfr <= 0) return;
-  float win[8];
-  cf tw1[8], tw2[8];
+    // ---------------------------------------------------------------- FFT rounds
+    const int nfr = min(NF, F - g * NF);  // valid frames in this segment
+    float2 *wbuf = reinterpret_cast<float2 *>(xbuf) + wave * kFftBuf;
+    const int nrounds = nfr > 0 ? (nfr + 7) / 8 : 0;
+    for (int rd = 0; rd < nrounds; ++rd) {
+      const int fa = 2 * (4 * rd + wave);
+      float pa[4], pb[4];
+      const bool active = fa < nfr;
+      if (active) {
+        cf v[8];
+        const float *fra = tile + WARM + 256 * fa;
 #pragma unroll
-  for (int r = 0; r < 8; ++r) {
-    win[r] = kHann512[lane + 64 * r];
-    const int i1 = (8 * r * (lane & 7)) & 511;
-    const int i2 = (r * lane) & 511;
-    tw1[r] = {kTwRe[i1], kTwIm[i1]};
-    tw2[r] = {kTwRe[i2], kTwIm[i2]};
-  }
-  float2 *wbuf = reinterpret_cast<float2 *>(xbuf) + wave * 512;
-  const int nrounds = (nfr + 7) / 8;
-  const int plane = (64 - lane) & 63;
-  for (int rd = 0; rd < nrounds; ++rd) {
-    const int fa = 2 * (4 * rd + wave);  // local frame index of z's real part
-    float pa[4], pb[4];
-    const bool active = fa < nfr;
-    if (active) {
-      cf v[8];
-      const float *fra = tile + WARM + 256 * fa;
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const int n = lane + 64 * r;
-        v[r] = {fra[n] * win[r], fra[256 + n] * win[r]};
-      }
-      fft512_wave(v, wbuf, lane, tw1, tw2);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float mr = __shfl(v[7 - r].r, plane, 64);
-        float mi = __shfl(v[7 - r].i, plane, 64);
-        if (lane == 0) {
-          mr = v[(8 - r) & 7].r;
-          mi = v[(8 - r) & 7].i;
+        for (int r = 0; r < 8; ++r) {
+          const int n = lane + 64 * r;
+          v[r] = {fra[n] * win[r], fra[256 + n] * win[r]};
         }
-        const float zr = v[r].r, zi = v[r].i;
-        pa[r] = 0.25f * ((zr + mr) * (zr + mr) + (zi - mi) * (zi - mi));
-        pb[r] = 0.25f * ((zi + mi) * (zi + mi) + (zr - mr) * (zr - mr));
-      }
-      if (lane == 0) {  // spec[:, :, 0] = 0 (PESQ.py:136)
-        pa[0] = 0.f;
-        pb[0] = 0.f;
-      }
-    }
-    __syncthreads();  // every wave is done reading the tile for this round
-    if (active) {
-      float *ra = tile + SPEC_LD * fa;
-      float *rb = ra + SPEC_LD;
+        fft512_wave(v, wbuf, lane, tw1, tw2);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        ra[lane + 64 * r] = pa[r];
-        rb[lane + 64 * r] = pb[r];
+        for (int r = 0; r < 4; ++r) {
+          float mr = __shfl(v[7 - r].r, plane, 64);
+          float mi = __shfl(v[7 - r].i, plane, 64);
+          if (lane == 0) {
+            mr = v[(8 - r) & 7].r;
+            mi = v[(8 - r) & 7].i;
+          }
+          const float zr = v[r].r, zi = v[r].i;
+          pa[r] = 0.25f * ((zr + mr) * (zr + mr) + (zi - mi) * (zi - mi));
+          pb[r] = 0.25f * ((zi + mi) * (zi + mi) + (zr - mr) * (zr - mr));
+        }
+        if (lane == 0) {  // spec[:, :, 0] = 0 (PESQ.py:136)
+          pa[0] = 0.f;
+          pb[0] = 0.f;
+        }
+      }
+      __syncthreads();  // every wave is done reading the tile for this round
+      STAMP(6 + rd);
+      if (active) {  // park the spectra in the consumed part of the tile
+        float *ra = tile + SPEC_LD * fa;
+        float *rb = ra + SPEC_LD;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          ra[lane + 64 * r] = pa[r];
+          rb[lane + 64 * r] = pb[r];
+        }
       }
     }
-    if ((rd & 1) || rd == nrounds - 1) {
-      // ---- Bark contraction of the 16-frame group on MFMA: C[frame][band] += P x Fb
-      __syncthreads();
-      const int grp = rd >> 1;
-      const int row = lane & 15, kq = lane >> 4;
-      const int frow = min(16 * grp + row, nfr - 1);
-      const float *srow = tile + SPEC_LD * frow;
-      // wave -> (small tile, part of tile 2) ; tile ranges from kBarkTileK
-      int tsmall, k0s, k1s, k02, k12;
-      if (wave == 0) { tsmall = 0; k02 = 14; k12 = 25; }
-      else if (wave == 1) { tsmall = 1; k02 = 25; k12 = 31; }
-      else if (wave == 2) { tsmall = -1; k02 = 31; k12 = 47; }
-      else { tsmall = 3; k02 = 47; k12 = 59; }
+    __syncthreads();
+    STAMP(13);
+
+    // ---------------------------------------------------------------- Bark bands on MFMA
+    if (16 * wave < nfr) {
       typedef float f4 __attribute__((ext_vector_type(4)));
-      f4 acc_s = {0.f, 0.f, 0.f, 0.f}, acc_2 = {0.f, 0.f, 0.f, 0.f};
-      if (tsmall >= 0) {
-        k0s = kBarkTileK[tsmall][0];
-        k1s = kBarkTileK[tsmall][1];
-        const int band = 16 * tsmall + row;
-        for (int kk = k0s; kk < k1s; ++kk) {
-          const int bin = 4 * kk + kq;
-          const float a = srow[bin];
-          const float bv = (band < NBARK && kBandOfBin[bin] == band) ? kBarkCorr[band] : 0.f;
-          acc_s = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bv, acc_s, 0, 0, 0);
-        }
-      }
-      {
-        const int band = 32 + row;
-        for (int kk = k02; kk < k12; ++kk) {
-          const int bin = 4 * kk + kq;
-          const float a = srow[bin];
-          const float bv = (kBandOfBin[bin] == band) ? kBarkCorr[band] : 0.f;
-          acc_2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bv, acc_2, 0, 0, 0);
-        }
-      }
-      // C/D layout: col = lane & 15 (band in tile), row = (lane >> 4) * 4 + i (frame)
-      float *part = xbuf + wave * 256;  // per-wave tile-2 partial (deterministic order)
+      const int row = lane & 15, kq = lane >> 4;
+      const float *srow = tile + SPEC_LD * min(16 * wave + row, nfr - 1);
+      f4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, c2a = c0, c2b = c0, c3 = c0;
+      // opaque copies: keep the 66 B-operand selects inside the item loop (else LICM hoists
+      // them all into live VGPRs across the whole kernel)
+      int blo[4], bhi[4];
+      float bcor[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) part[(kq * 4 + i) * 16 + row] = acc_2[i];
-      if (tsmall >= 0) {
-        const int band = 16 * tsmall + row;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int fl = 16 * grp + kq * 4 + i;
-          if (band < NBARK && fl < nfr)
-            bark[((int64_t)s * F + (int64_t)g * NF + fl) * NBARK + band] = acc_s[i];
+      for (int t = 0; t < 4; ++t) {
+        blo[t] = blo_c[t];
+        bhi[t] = bhi_c[t];
+        bcor[t] = bcor_c[t];
+        asm volatile("" : "+v"(blo[t]), "+v"(bhi[t]), "+v"(bcor[t]));
+      }
+      for (int kk = kBarkTileK[0][0]; kk < kBarkTileK[0][1]; ++kk) {
+        const int bin = 4 * kk + kq;
+        c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(srow[bin], (bin >= blo[0] && bin < bhi[0]) ? bcor[0] : 0.f, c0, 0, 0, 0);
+      }
+      for (int kk = kBarkTileK[1][0]; kk < kBarkTileK[1][1]; ++kk) {
+        const int bin = 4 * kk + kq;
+        c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(srow[bin], (bin >= blo[1] && bin < bhi[1]) ? bcor[1] : 0.f, c1, 0, 0, 0);
+      }
+      for (int kk = kBarkTileK[2][0]; kk < kBarkTileK[2][1]; kk += 2) {
+        const int bin = 4 * kk + kq;
+        c2a = __builtin_amdgcn_mfma_f32_16x16x4f32(srow[bin], (bin >= blo[2] && bin < bhi[2]) ? bcor[2] : 0.f, c2a, 0, 0, 0);
+        if (kk + 1 < kBarkTileK[2][1]) {
+          const int bin2 = bin + 4;
+          c2b = __builtin_amdgcn_mfma_f32_16x16x4f32(srow[bin2], (bin2 >= blo[2] && bin2 < bhi[2]) ? bcor[2] : 0.f, c2b, 0, 0, 0);
         }
       }
-      __syncthreads();
-      {
-        const int fr_ = tid >> 4, col = tid & 15;
-        const float v = xbuf[tid] + xbuf[256 + tid] + xbuf[512 + tid] + xbuf[768 + tid];
-        const int fl = 16 * grp + fr_;
-        if (fl < nfr) bark[((int64_t)s * F + (int64_t)g * NF + fl) * NBARK + 32 + col] = v;
+      for (int kk = kBarkTileK[3][0]; kk < kBarkTileK[3][1]; ++kk) {
+        const int bin = 4 * kk + kq;
+        c3 = __builtin_amdgcn_mfma_f32_16x16x4f32(srow[bin], (bin >= blo[3] && bin < bhi[3]) ? bcor[3] : 0.f, c3, 0, 0, 0);
       }
-      __syncthreads();
+      // C/D: col = lane & 15 (band in tile), row = 4 * (lane >> 4) + i (frame in group)
+      float *brow = bark + ((int64_t)it.s * F + (int64_t)g * NF + 16 * wave) * NBARK;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int fl = 16 * wave + 4 * kq + i;
+        if (fl < nfr) {
+          float *o = brow + (4 * kq + i) * NBARK;
+          o[row] = c0[i];
+          o[16 + row] = c1[i];
+          o[32 + row] = c2a[i] + c2b[i];
+          if (row == 0) o[48] = c3[i];
+        }
+      }
     }
+    __syncthreads();  // tile is rewritten by the next item
+    STAMP(15);
   }
 }
 
@@ -343,27 +418,46 @@ __global__ void __launch_bounds__(256) pesq_power_sum(const float *__restrict__ 
 }
 
 // ------------------------------------------------------------------------------ back end
+// x^e for x > 0 (every call site: x >= 0.5 or a ratio of positive terms) via the hardware
+// v_log_f32 / v_exp_f32 (~1 ulp each); the reference evaluates these in float64, the
+// difference is ~1e-7 relative, far inside the +-0.01 MOS tolerance.
+__device__ __forceinline__ float pow_pos(float x, float e) {
+  return __builtin_amdgcn_exp2f(e * __builtin_amdgcn_logf(x));
+}
+
 __device__ __forceinline__ float loud(float p, int b) {
   // loudness.py:64-65: (2T)^e ((0.5 + 0.5 P/T)^e - 1), 0 where P <= T; times Sl (folded)
   const float t = kThresh[b];
   if (!(p > t)) return 0.f;
-  return kLoud2TE[b] * (powf(fmaf(0.5f, p / t, 0.5f), kLoudExp[b]) - 1.f);
+  return kLoud2TE[b] * (pow_pos(fmaf(0.5f, p / t, 0.5f), kLoudExp[b]) - 1.f);
 }
 
-__global__ void __launch_bounds__(256)
+// Frames are processed in chunks of BC staged in LDS by coalesced loads ([frame][49] rows are
+// contiguous per signal); lane = frame for the per-frame math, lane = band for band sums.
+constexpr int BT = 128;   // threads per workgroup
+constexpr int BC = BT;    // frames per chunk
+constexpr int BLD = 49;   // odd row stride: lane = frame reads are bank-conflict-free
+
+__device__ __forceinline__ void stage_chunk(float *__restrict__ dst, const float *__restrict__ src, int nf,
+                                            int tid) {
+  const int n = nf * NBARK;
+  for (int i = tid; i < n; i += BT) dst[i] = src[i];
+}
+
+__global__ void __launch_bounds__(BT)
     pesq_back(const float *__restrict__ bark, const float *__restrict__ power, int64_t B, int64_t L,
               int F, float *__restrict__ scratch, float *__restrict__ mos) {
+  __shared__ float C[BC * BLD], N[BC * BLD];
   __shared__ float ratio[NBARK];
-  __shared__ double dred[8];
-  __shared__ float fred[8];
-  __shared__ float bsum[4][2][64];
+  __shared__ float frs[BC + 1];
+  __shared__ double dred[4];
+  __shared__ float bsum[2][2][64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t b = blockIdx.x;
   const float *__restrict__ bc = bark + (b * (int64_t)F) * NBARK;
   const float *__restrict__ bn = bark + ((b + B) * (int64_t)F) * NBARK;
-  float *__restrict__ silent = scratch + b * (int64_t)F * 5;
-  float *__restrict__ fr = silent + F;
-  float *__restrict__ afpc = fr + F;
+  float *__restrict__ silent = scratch + b * (int64_t)F * 4;
+  float *__restrict__ afpc = silent + F;
   float *__restrict__ sym = afpc + F;
   float *__restrict__ asym = sym + F;
   // PESQ.py:97-100 -- power = sum / (L + 5120) / 1.04684; bark scales by 1e7 / power
@@ -371,84 +465,103 @@ __global__ void __launch_bounds__(256)
   const float pn = power[b + B] / (float)(L + 5120) / 1.04684f;
   const float sc = 1e7f / pc, sn = 1e7f / pn;
 
-  // pass 1: silent frames (PESQ.py:146, loudness.py:48-53 with factor 1e2)
-  for (int f = tid; f < F; f += 256) {
-    float a = 0.f;
-    for (int k = 0; k < NBARK; ++k) {
-      const float c = bc[f * NBARK + k] * sc;
-      a += (c > kThresh[k] * 100.f) ? c : 0.f;
+  // ---- pass 1: silent frames (PESQ.py:146, loudness.py:48-53 x 1e2) + band means (:55-60)
+  float mc = 0.f, mn = 0.f;
+  for (int f0 = 0; f0 < F; f0 += BC) {
+    const int nf = min(BC, F - f0);
+    __syncthreads();
+    stage_chunk(C, bc + (int64_t)f0 * NBARK, nf, tid);
+    stage_chunk(N, bn + (int64_t)f0 * NBARK, nf, tid);
+    __syncthreads();
+    if (tid < nf) {
+      float a = 0.f;
+#pragma unroll 7
+      for (int k = 0; k < NBARK; ++k) {
+        const float c = C[tid * BLD + k] * sc;
+        a += (c > kThresh[k] * 100.f) ? c : 0.f;
+      }
+      const float sil = (a < 1e7f) ? 1.f : 0.f;
+      frs[tid] = sil;
+      silent[f0 + tid] = sil;
     }
-    silent[f] = (a < 1e7f) ? 1.f : 0.f;
-  }
-  __syncthreads();
-  // pass 2: mean audible band power over all frames (loudness.py:55-60)
-  {
-    float mc = 0.f, mn = 0.f;
+    __syncthreads();
     if (lane < NBARK) {
       const float t100 = kThresh[lane] * 100.f;
-      for (int f = wave; f < F; f += 4) {
-        if (silent[f] != 0.f) continue;
-        const float c = bc[f * NBARK + lane] * sc;
-        const float n = bn[f * NBARK + lane] * sn;
+      for (int f = wave; f < nf; f += 2) {
+        if (frs[f] != 0.f) continue;
+        const float c = C[f * BLD + lane] * sc;
+        const float n = N[f * BLD + lane] * sn;
         mc += (c > t100) ? c : 0.f;
         mn += (n > t100) ? n : 0.f;
       }
     }
-    bsum[wave][0][lane] = mc;
-    bsum[wave][1][lane] = mn;
-    __syncthreads();
-    if (tid < NBARK) {
-      const float c = (bsum[0][0][tid] + bsum[1][0][tid] + bsum[2][0][tid] + bsum[3][0][tid]) / F;
-      const float n = (bsum[0][1][tid] + bsum[1][1][tid] + bsum[2][1][tid] + bsum[3][1][tid]) / F;
-      ratio[tid] = fminf(fmaxf((n + 1000.f) / (c + 1000.f), 0.01f), 100.f);  // PESQ.py:151-152
-    }
-    __syncthreads();
   }
-  // pass 3: frame power ratio (PESQ.py:157-159)
-  for (int f = tid; f < F; f += 256) {
-    float ac = 0.f, an = 0.f;
-    for (int k = 0; k < NBARK; ++k) {
-      const float c = ratio[k] * (bc[f * NBARK + k] * sc);
-      const float n = bn[f * NBARK + k] * sn;
-      ac += (c > kThresh[k]) ? c : 0.f;
-      an += (n > kThresh[k]) ? n : 0.f;
-    }
-    fr[f] = (ac + 5e3f) / (an + 5e3f);
-    afpc[f] = ac;
-  }
+  bsum[wave][0][lane] = mc;
+  bsum[wave][1][lane] = mn;
   __syncthreads();
-  // pass 4: loudness, disturbances, weighting (PESQ.py:161-224)
+  if (tid < NBARK) {
+    const float c = (bsum[0][0][tid] + bsum[1][0][tid]) / F;
+    const float n = (bsum[0][1][tid] + bsum[1][1][tid]) / F;
+    ratio[tid] = fminf(fmaxf((n + 1000.f) / (c + 1000.f), 0.01f), 100.f);  // PESQ.py:151-152
+  }
+
+  // ---- pass 2: frame ratio (PESQ.py:157-163), loudness, disturbances (PESQ.py:186-224)
   const float sqrt_tw = sqrtf((float)kTotalWidth);
-  for (int f = tid; f < F; f += 256) {
-    float r = (f >= 1) ? 0.8f * fr[f] + 0.2f * fr[f - 1] : fr[0];  // non-recursive (PESQ.py:161)
-    r = fminf(fmaxf(r, 3e-4f), 5.f);
-    float s2 = 0.f, as = 0.f;
-    for (int k = 0; k < NBARK; ++k) {
-      const float ec = ratio[k] * (bc[f * NBARK + k] * sc);
-      const float en = r * (bn[f * NBARK + k] * sn);
-      const float lc = loud(ec, k), ln = loud(en, k);
-      float d = ln - lc;
-      const float dz = 0.25f * fminf(lc, ln);
-      d = copysignf(fmaxf(fabsf(d) - dz, 0.f), d);
-      if (k >= 1) {
-        const float wd = kWidthBark[k] * d;
-        s2 = fmaf(wd, wd, s2);
-        float a = powf((en + 50.f) / (ec + 50.f), 1.2f);
-        a = (a < 3.f) ? 0.f : fminf(a, 12.f);
-        as += fabsf(wd * a);
+  float fr_prev = 0.f;  // frame power ratio of the last frame of the previous chunk
+  for (int f0 = 0; f0 < F; f0 += BC) {
+    const int nf = min(BC, F - f0);
+    __syncthreads();
+    stage_chunk(C, bc + (int64_t)f0 * NBARK, nf, tid);
+    stage_chunk(N, bn + (int64_t)f0 * NBARK, nf, tid);
+    __syncthreads();
+    float ac = 0.f;
+    if (tid < nf) {
+      float an = 0.f;
+#pragma unroll 7
+      for (int k = 0; k < NBARK; ++k) {
+        const float c = ratio[k] * (C[tid * BLD + k] * sc);
+        const float n = N[tid * BLD + k] * sn;
+        ac += (c > kThresh[k]) ? c : 0.f;
+        an += (n > kThresh[k]) ? n : 0.f;
       }
+      frs[tid + 1] = (ac + 5e3f) / (an + 5e3f);
     }
-    float sy = fmaxf(sqrt_tw * sqrtf(s2), 1e-20f);
-    float ay = fmaxf(as, 1e-20f);
-    const float w = powf((afpc[f] + 1e5f) / 1e7f, 0.04f);
-    sym[f] = fminf(sy / w, 45.f);
-    asym[f] = fminf(ay / w, 45.f);
+    if (tid == 0) frs[0] = fr_prev;
+    __syncthreads();
+    fr_prev = frs[nf];
+    if (tid < nf) {
+      const int f = f0 + tid;
+      float r = (f >= 1) ? 0.8f * frs[tid + 1] + 0.2f * frs[tid] : frs[1];  // non-recursive (PESQ.py:161)
+      r = fminf(fmaxf(r, 3e-4f), 5.f);
+      float s2 = 0.f, as = 0.f;
+#pragma unroll 1
+      for (int k = 0; k < NBARK; ++k) {
+        const float ec = ratio[k] * (C[tid * BLD + k] * sc);
+        const float en = r * (N[tid * BLD + k] * sn);
+        const float lc = loud(ec, k), ln = loud(en, k);
+        float d = ln - lc;
+        const float dz = 0.25f * fminf(lc, ln);
+        d = copysignf(fmaxf(fabsf(d) - dz, 0.f), d);
+        if (k >= 1) {
+          const float wd = kWidthBark[k] * d;
+          s2 = fmaf(wd, wd, s2);
+          float a = pow_pos((en + 50.f) / (ec + 50.f), 1.2f);
+          a = (a < 3.f) ? 0.f : fminf(a, 12.f);
+          as += fabsf(wd * a);
+        }
+      }
+      const float sy = fmaxf(sqrt_tw * sqrtf(s2), 1e-20f);
+      const float ay = fmaxf(as, 1e-20f);
+      const float w = pow_pos((ac + 1e5f) / 1e7f, 0.04f);
+      sym[f] = fminf(sy / w, 45.f);
+      asym[f] = fminf(ay / w, 45.f);
+    }
   }
   __syncthreads();
-  // pass 5: L6 within 20-frame windows (hop 10), L2 across windows (PESQ.py:168-172)
+  // ---- pass 3: L6 within 20-frame windows (hop 10), L2 across windows (PESQ.py:168-172)
   const int nw = (F - 20) / 10 + 1;
   double as_ = 0.0, aa_ = 0.0;
-  for (int w = tid; w < nw; w += 256) {
+  for (int w = tid; w < nw; w += BT) {
     double s6 = 0.0, a6 = 0.0;
     for (int i = 0; i < 20; ++i) {
       const double x = sym[10 * w + i], y = asym[10 * w + i];
@@ -460,16 +573,21 @@ __global__ void __launch_bounds__(256)
     as_ += ps * ps;
     aa_ += pa * pa;
   }
-  as_ = block_sum_256_d(as_, dred);
+  as_ = wave_sum_d(as_);
+  aa_ = wave_sum_d(aa_);
+  if (lane == 0) {
+    dred[2 * wave] = as_;
+    dred[2 * wave + 1] = aa_;
+  }
   __syncthreads();
-  aa_ = block_sum_256_d(aa_, dred + 4);
+  as_ = dred[0] + dred[2];
+  aa_ = dred[1] + dred[3];
   if (tid == 0) {
     const double ds = sqrt(as_ / nw), da = sqrt(aa_ / nw);
-    double m = 4.5 - 0.1 * ds - 0.0309 * da;           // PESQ.py:240
+    double m = 4.5 - 0.1 * ds - 0.0309 * da;              // PESQ.py:240
     m = 0.999 + 4.0 / (1.0 + exp(-1.3669 * m + 3.8224));  // PESQ.py:243
     mos[b] = (float)m;
   }
-  (void)fred;
 }
 
 inline int frames_of(int64_t L) {
@@ -498,6 +616,15 @@ using namespace fsem;
 
 extern "C" int fsem_pesq_frames(int64_t length) { return pesq::frames_of(length); }
 
+#ifdef FSEM_STAMPS
+// diagnostic build only (not part of include/fsem.h)
+extern "C" int fsem_debug_read_stamps(void *dst, size_t bytes) {
+  if (hipDeviceSynchronize() != hipSuccess) return FSEM_ELAUNCH;
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(pesq::g_stamps), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess
+             ? FSEM_OK : FSEM_ELAUNCH;
+}
+#endif
+
 extern "C" size_t fsem_pesq_front_workspace_bytes(int64_t batch, int64_t length) {
   const pesq::Geometry g = pesq::geometry(length);
   return align_up(sizeof(float) * (size_t)(2 * batch) * (size_t)g.nseg, 256);
@@ -519,12 +646,14 @@ extern "C" int fsem_pesq_front_f32(const float *ref, const float *deg, int64_t b
   const pesq::Geometry g = pesq::geometry(length);
   if (g.F < 20) return FSEM_ESHORT;
   if (ws_bytes < fsem_pesq_front_workspace_bytes(batch, length) || !ws) return FSEM_EWORKSPACE;
-  const int64_t nblk = 2 * batch * (int64_t)g.nseg;
-  if (nblk > 0x7fffffff) return FSEM_EINVAL;
+  const int64_t nitems = 2 * batch * (int64_t)g.nseg;
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  const int64_t grid = std::min<int64_t>(nitems, (int64_t)ncu * 2);  // 2 resident workgroups per CU
   float *ppart = static_cast<float *>(ws);
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(pesq::pesq_front, dim3((unsigned)nblk), dim3(pesq::PT), 0, st, ref, deg, batch,
-                     length, ld, g.F, g.nseg, g.npseg, bark, ppart);
+  hipLaunchKernelGGL(pesq::pesq_front, dim3((unsigned)grid), dim3(pesq::PT), 0, st, ref, deg, batch,
+                     length, ld, g.F, g.nseg, g.npseg, nitems, bark, ppart);
   FSEM_CHECK_LAUNCH();
   hipLaunchKernelGGL(pesq::pesq_power_sum, dim3((unsigned)((2 * batch + 255) / 256)), dim3(256), 0, st,
                      ppart, g.nseg, 2 * batch, power);
@@ -534,7 +663,7 @@ extern "C" int fsem_pesq_front_f32(const float *ref, const float *deg, int64_t b
 
 extern "C" size_t fsem_pesq_back_workspace_bytes(int64_t batch, int64_t length) {
   const pesq::Geometry g = pesq::geometry(length);
-  return align_up(sizeof(float) * (size_t)batch * (size_t)g.F * 5, 256);
+  return align_up(sizeof(float) * (size_t)batch * (size_t)g.F * 4, 256);
 }
 
 extern "C" int fsem_pesq_back_f32(const float *bark, const float *power, int64_t batch, int64_t length,
@@ -544,7 +673,7 @@ extern "C" int fsem_pesq_back_f32(const float *bark, const float *power, int64_t
   if (g.F < 20) return FSEM_ESHORT;
   if (!ws || ws_bytes < fsem_pesq_back_workspace_bytes(batch, length)) return FSEM_EWORKSPACE;
   if (batch > 0x7fffffff) return FSEM_EINVAL;
-  hipLaunchKernelGGL(pesq::pesq_back, dim3((unsigned)batch), dim3(256), 0, (hipStream_t)stream, bark,
+  hipLaunchKernelGGL(pesq::pesq_back, dim3((unsigned)batch), dim3(pesq::BT), 0, (hipStream_t)stream, bark,
                      power, batch, length, g.F, static_cast<float *>(ws), mos);
   FSEM_CHECK_LAUNCH();
   return FSEM_OK;

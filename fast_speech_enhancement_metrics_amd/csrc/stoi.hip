@@ -42,63 +42,146 @@ __device__ __forceinline__ float sample10(const Src &s, int64_t o, int64_t L10, 
   return direct ? s.x[o] : resample_at(s.x, s.n, o, rk);
 }
 
-// Resample both signals of an utterance to 10 kHz once (written to the workspace, read
-// back only for the kept frames by stoi_tob) and compute the clean frame energies of this
-// chunk of VF frames.  Mode 0: 16 -> 10 kHz polyphase with the compile-time torchaudio
-// kernel kRs16k10k (each lane: one 8-in / 5-out group, 28 LDS reads, 140 FMAs with
-// uniform coefficients); mode 1: input already at 10 kHz; mode 2: generic rate pair.
-constexpr int VF2 = 32;                 // VAD frames per workgroup
-constexpr int YT = VF2 * 128 + 128;     // 10 kHz samples staged per workgroup
-constexpr int XT = (YT / 5 + 2) * 8 + 28;  // 16 kHz samples staged (mode 0)
+// Resample both signals of an utterance to 10 kHz once (written to the workspace, read back
+// only for the kept frames by stoi_tob) and compute the clean frame energies (STOI.py:92-99).
+// Persistent workgroups walk items (utterance, chunk, signal); the next item's 16 kHz input is
+// in flight in registers (range-checked buffer loads) while the current one is resampled.
+// 16 -> 10 kHz: each lane evaluates one polyphase group (8 inputs in, 5 outputs out) with the
+// compile-time torchaudio kernel kRs16k10k (28 LDS reads, 140 uniform-coefficient FMAs).
+constexpr int VF2 = 32;                        // VAD frames per chunk
+constexpr int YT = VF2 * 128 + 128;            // 10 kHz samples produced per item (8320)
+constexpr int NG = YT / 5 + 2;                 // polyphase groups per item
+constexpr int XT4 = (8 * NG + 32) / 4;         // float4s of 16 kHz input staged per item
+constexpr int XPF = (XT4 + 255) / 256;         // prefetch float4s per thread
+__global__ void __launch_bounds__(256, 2)
+    stoi_resample_vad16(const float *__restrict__ ref, const float *__restrict__ deg, int64_t n_in, int64_t ld,
+                        int64_t L10, int NV, int nchunk, int64_t nitems, float *__restrict__ y10, int64_t y_ld,
+                        float *__restrict__ energy, int nv_ld) {
+  __shared__ __attribute__((aligned(16))) float xin[XPF * 256 * 4];
+  __shared__ __attribute__((aligned(16))) float ytile[YT + 8];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t nbytes = (uint32_t)(((n_in + 3) & ~(int64_t)3) * 4);
+  auto item_src = [&](int64_t item, int64_t &b, int &chunk, int &sig, int64_t &o0, int64_t &i0) {
+    sig = (int)(item & 1);
+    const int64_t bc = item >> 1;
+    b = bc / nchunk;
+    chunk = (int)(bc - b * nchunk);
+    o0 = (int64_t)chunk * (VF2 * 128);
+    i0 = 8 * (o0 / 5) - 12;  // 4-aligned base; group m reads x[8m - 10 + t] = xin[8(m - m0) + 2 + t]
+  };
+  auto prefetch = [&](int64_t item, float4 pre[XPF]) {
+    int64_t b, o0, i0;
+    int chunk, sig;
+    item_src(item, b, chunk, sig, o0, i0);
+    const float *row = (sig == 0 ? ref : deg) + b * ld;
+    const uint64_t base = reinterpret_cast<uint64_t>(row);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
+    void *p = reinterpret_cast<void *>(((uint64_t)hi << 32) | lo);
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc(p, 0, __builtin_amdgcn_readfirstlane(nbytes), 0x00020000);
+#pragma unroll
+    for (int k = 0; k < XPF; ++k) {
+      const int64_t t = i0 + 4 * (tid + 256 * k);
+      typedef float v4f __attribute__((ext_vector_type(4)));
+      v4f v = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(t * 4), 0, 0));
+      // zero-pad past the row end (torchaudio pads the input, base.py:20)
+      if (t + 3 >= n_in) {
+        v.x = (t < n_in) ? v.x : 0.f;
+        v.y = (t + 1 < n_in) ? v.y : 0.f;
+        v.z = (t + 2 < n_in) ? v.z : 0.f;
+        v.w = 0.f;
+      }
+      pre[k] = make_float4(v.x, v.y, v.z, v.w);
+    }
+  };
+  float4 pre[XPF];
+  int64_t item = blockIdx.x;
+  if (item < nitems) prefetch(item, pre);
+  for (; item < nitems; item += gridDim.x) {
+    int64_t b, o0, i0;
+    int chunk, sig;
+    item_src(item, b, chunk, sig, o0, i0);
+    float4 *x4 = reinterpret_cast<float4 *>(xin);
+#pragma unroll
+    for (int k = 0; k < XPF; ++k) x4[tid + 256 * k] = pre[k];
+    __syncthreads();
+    if (item + gridDim.x < nitems) prefetch(item + gridDim.x, pre);
+    const int64_t o_end = min(o0 + (int64_t)YT, L10);
+    const int64_t m0 = o0 / 5;
+    const int64_t m1 = (o_end + 4) / 5;
+    for (int64_t m = m0 + tid; m < m1; m += 256) {
+      const float2 *xs2 = reinterpret_cast<const float2 *>(xin + 8 * (m - m0) + 2);
+      float v[28];
+#pragma unroll
+      for (int t = 0; t < 14; ++t) {
+        const float2 q = xs2[t];
+        v[2 * t] = q.x;
+        v[2 * t + 1] = q.y;
+      }
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        float acc = 0.f;
+#pragma unroll
+        for (int t = 0; t < 28; ++t) acc = fmaf(kRs16k10k[j][t], v[t], acc);
+        const int64_t o = 5 * m + j;
+        if (o >= o0 && o < o_end) ytile[o - o0] = acc;
+      }
+    }
+    __syncthreads();
+    // store this chunk's own 10 kHz samples (float4, coalesced; y_ld % 64 == 0, o0 % 4 == 0)
+    const int nown = (int)min((int64_t)(VF2 * 128), L10 - o0);
+    float *__restrict__ yr = y10 + (b * 2 + sig) * y_ld + o0;
+    for (int k = tid; 4 * k < nown; k += 256) {
+      if (4 * k + 3 < nown) {
+        reinterpret_cast<float4 *>(yr)[k] = reinterpret_cast<const float4 *>(ytile)[k];
+      } else {
+        for (int c = 4 * k; c < nown; ++c) yr[c] = ytile[c];
+      }
+    }
+    if (sig == 0) {
+      // frame energies 20 log10(||w * frame|| + 1e-9) (STOI.py:92-99)
+      for (int f = wave; f < VF2; f += 4) {
+        const int i = chunk * VF2 + f;
+        if (i >= NV) break;
+        const float *fr = ytile + 128 * f;
+        float acc = 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = kHann256s[lane + 64 * r] * fr[lane + 64 * r];
+          acc = fmaf(v, v, acc);
+        }
+        acc = wave_sum(acc);
+        if (lane == 0) energy[b * nv_ld + i] = 20.f * log10f(sqrtf(acc) + 1e-9f);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Generic rate pairs (and 10 kHz input): one output per thread through resample_at.
+constexpr int VF3 = 32;
+constexpr int YT3 = VF3 * 128 + 128;
 __global__ void __launch_bounds__(256)
     stoi_resample_vad(const float *__restrict__ ref, const float *__restrict__ deg, int64_t n_in, int64_t ld,
                       int64_t L10, int NV, int mode, ResampleKernel rk, float *__restrict__ y10, int64_t y_ld,
                       float *__restrict__ energy, int nv_ld) {
-  __shared__ __attribute__((aligned(16))) float xin[XT];
-  __shared__ __attribute__((aligned(16))) float ytile[YT];
+  __shared__ __attribute__((aligned(16))) float ytile[YT3];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t b = blockIdx.y;
-  const int64_t o0 = (int64_t)blockIdx.x * (VF2 * 128);
-  const int64_t o_end = min(o0 + (int64_t)YT, L10);
+  const int64_t o0 = (int64_t)blockIdx.x * (VF3 * 128);
+  const int64_t o_end = min(o0 + (int64_t)YT3, L10);
   const int ny = (int)(o_end - o0);
-  const int nw_own = (int)min((int64_t)(VF2 * 128), L10 - o0);
+  const int nw_own = (int)min((int64_t)(VF3 * 128), L10 - o0);
   for (int sig = 0; sig < 2; ++sig) {
-    const float *__restrict__ x = (sig == 0 ? ref : deg) + b * ld;
-    if (mode == 0) {
-      const int64_t m0 = o0 / 5;
-      const int64_t m1 = (o_end + 4) / 5;
-      const int64_t i0 = 8 * m0 - 10;
-      const int nin = (int)(8 * (m1 - m0) + 20);
-      for (int k = tid; k < nin; k += 256) {
-        const int64_t i = i0 + k;
-        xin[k] = (i >= 0 && i < n_in) ? x[i] : 0.f;
-      }
-      __syncthreads();
-      for (int64_t m = m0 + tid; m < m1; m += 256) {
-        const float *xs = xin + 8 * (m - m0);
-        float v[28];
-#pragma unroll
-        for (int t = 0; t < 28; ++t) v[t] = xs[t];
-#pragma unroll
-        for (int j = 0; j < 5; ++j) {
-          float acc = 0.f;
-#pragma unroll
-          for (int t = 0; t < 28; ++t) acc = fmaf(kRs16k10k[j][t], v[t], acc);
-          const int64_t o = 5 * m + j;
-          if (o >= o0 && o < o_end) ytile[o - o0] = acc;
-        }
-      }
-    } else {
-      const Src src{x, n_in};
-      for (int k = tid; k < ny; k += 256) ytile[k] = sample10(src, o0 + k, L10, mode == 1, rk);
-    }
+    const Src src{(sig == 0 ? ref : deg) + b * ld, n_in};
+    for (int k = tid; k < ny; k += 256) ytile[k] = sample10(src, o0 + k, L10, mode == 1, rk);
     __syncthreads();
     float *__restrict__ yr = y10 + (b * 2 + sig) * y_ld + o0;
     for (int k = tid; k < nw_own; k += 256) yr[k] = ytile[k];
     if (sig == 0) {
-      // frame energies 20 log10(||w * frame|| + 1e-9) (STOI.py:92-99)
-      for (int f = wave; f < VF2; f += 4) {
-        const int i = blockIdx.x * VF2 + f;
+      for (int f = wave; f < VF3; f += 4) {
+        const int i = blockIdx.x * VF3 + f;
         if (i >= NV) break;
         const float *fr = ytile + 128 * f;
         float acc = 0.f;
@@ -148,7 +231,7 @@ __global__ void __launch_bounds__(256)
     stoi_tob(const float *__restrict__ y10, int64_t y_ld, int64_t B, int64_t L10, const int *__restrict__ idx,
              const int *__restrict__ kept, int nv_ld, float *__restrict__ tob, int64_t tmax) {
   __shared__ __attribute__((aligned(16))) float blk[2][TF + 1][128];
-  __shared__ __attribute__((aligned(16))) float xbuf[4 * 1024];
+  __shared__ __attribute__((aligned(16))) float xbuf[4 * 2 * kFftBuf];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t b = blockIdx.y;
   const int n = kept[b];
@@ -197,7 +280,7 @@ __global__ void __launch_bounds__(256)
   cf tw1[8], tw2[8];
   fft512_twiddles(lane, tw1, tw2);
   const float win[4] = {w_lo, w_lo2, w_hi, w_hi2};  // STFT window on the 256 centred samples
-  float2 *wbuf = reinterpret_cast<float2 *>(xbuf) + wave * 512;
+  float2 *wbuf = reinterpret_cast<float2 *>(xbuf) + wave * kFftBuf;
   float *pbuf = reinterpret_cast<float *>(wbuf);
   const int plane = (64 - lane) & 63;
   for (int k = k0 + wave; k < kend; k += 4) {
@@ -432,8 +515,19 @@ inline int run(const float *ref, const float *deg, int64_t B, int64_t length, in
   if (kept_out) kept = kept_out;
   float *y10 = reinterpret_cast<float *>(reinterpret_cast<char *>(ws) + ws_bytes(B, g) -
                                          align_up(sizeof(float) * (size_t)(2 * B) * (size_t)g.y_ld, 256));
-  hipLaunchKernelGGL(stoi_resample_vad, dim3((unsigned)((g.L10 + VF2 * 128 - 1) / (VF2 * 128)), (unsigned)B),
-                     dim3(256), 0, st, ref, deg, length, ld, g.L10, g.NV, g.mode, rk, y10, g.y_ld, energy, g.nv_ld);
+  if (g.mode == 0) {
+    const int nchunk = (int)((g.L10 + VF2 * 128 - 1) / (VF2 * 128));
+    const int64_t nitems = B * (int64_t)nchunk * 2;
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const int64_t grid = nitems < (int64_t)ncu * 3 ? nitems : (int64_t)ncu * 3;  // 3 resident per CU
+    hipLaunchKernelGGL(stoi_resample_vad16, dim3((unsigned)grid), dim3(256), 0, st, ref, deg, length, ld, g.L10,
+                       g.NV, nchunk, nitems, y10, g.y_ld, energy, g.nv_ld);
+  } else {
+    hipLaunchKernelGGL(stoi_resample_vad, dim3((unsigned)((g.L10 + VF3 * 128 - 1) / (VF3 * 128)), (unsigned)B),
+                       dim3(256), 0, st, ref, deg, length, ld, g.L10, g.NV, g.mode, rk, y10, g.y_ld, energy,
+                       g.nv_ld);
+  }
   FSEM_CHECK_LAUNCH();
   hipLaunchKernelGGL(stoi_select, dim3((unsigned)B), dim3(256), 0, st, energy, g.nv_ld, g.NV, idx, kept);
   FSEM_CHECK_LAUNCH();

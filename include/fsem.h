@@ -14,7 +14,9 @@
  *  - the library allocates nothing: scratch space comes from `ws` (size from the
  *    matching *_workspace_bytes query); work is enqueued asynchronously on `stream`
  *    (a hipStream_t; NULL = the default stream) and the call returns immediately;
- *  - signals are float32 rows: element (b, t) of a batch lives at ptr[b * ld + t];
+ *  - signals are float32 rows: element (b, t) of a batch lives at ptr[b * ld + t]; the
+ *    PESQ and STOI entries read rows in 16-byte pieces, so each row must be readable up to
+ *    ceil4(length) floats (values past `length` are never used);
  *  - return 0 on success or a negative FSEM_E* code (fsem_strerror() for text);
  *  - re-entrant across streams / devices (launches use the current HIP device).
  */

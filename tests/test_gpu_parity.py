@@ -43,11 +43,14 @@ def test_pesq_front_bark_matches_reference(dev, name):
     c = torch.from_numpy(g["clean_f"]).to(dev)
     n = torch.from_numpy(g["noisy_f"]).to(dev)
     B, L = c.shape
+    c = torch.nn.functional.pad(c, (0, (-L) % 4)).contiguous()  # rows readable to ceil4(L)
+    n = torch.nn.functional.pad(n, (0, (-L) % 4)).contiguous()
+    ld = c.shape[1]
     F = lib.fsem_pesq_frames(L)
     bark = torch.empty(2 * B, F, 49, device=dev)
     power = torch.empty(2 * B, device=dev)
     ws = _native.workspace(lib.fsem_pesq_front_workspace_bytes(B, L), dev)
-    _native.check(lib.fsem_pesq_front_f32(c.data_ptr(), n.data_ptr(), B, L, L, bark.data_ptr(), power.data_ptr(),
+    _native.check(lib.fsem_pesq_front_f32(c.data_ptr(), n.data_ptr(), B, L, ld, bark.data_ptr(), power.data_ptr(),
                                           ws.data_ptr(), ws.numel(), _native.stream_handle(dev)), "front")
     torch.cuda.synchronize()
     p = power.double().cpu().numpy() / (L + 5120) / 1.04684
