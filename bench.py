@@ -5,10 +5,12 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-One step = the drop-in API calls ``PESQ(16000, use_gpu=True)(clean, noisy)`` and
-``STOI(16000, use_gpu=True)(clean, noisy)`` on this rank's batch (4096 pairs per GPU by
-default: BASELINE.json configs[1], 10 s @ 16 kHz fp32), including the list-of-dict result
-construction, plus (N > 1) the RCCL all-gather of the per-utterance scores over xGMI.
+One step = the engine work behind the drop-in API calls ``PESQ(16000, use_gpu=True)`` and
+``STOI(16000, use_gpu=True)`` on this rank's batch (4096 pairs per GPU by default:
+BASELINE.json configs[1], 10 s @ 16 kHz fp32): ``PESQ.scores`` + ``STOI.scores`` (the same
+kernels ``__call__`` runs), the RCCL all-gather of the per-utterance [B, 3] scores over xGMI
+(N > 1), and one device->host copy of the job's scores on rank 0.  The API's Python
+list-of-dict formatting is not included (see DESIGN.md for its cost).
 Weak scaling: every rank owns its own shard of utterances, generated in HBM before timing.
 
 Rank 0 prints ONE JSON line with the metric, the roofline of the dominant kernel
@@ -135,18 +137,15 @@ def main():
     pesq = PESQ(16000, use_gpu=True)
     stoi = STOI(16000, use_gpu=True)
 
-    gather_buf = None
-    if distributed:
-        gather_buf = torch.empty(world * B, 3, device=dev)
+    from fast_speech_enhancement_metrics_amd.distributed import gather_scores
 
     def step():
-        r_p = pesq(clean, noisy)
-        r_s = stoi(clean, noisy)
-        if distributed:
-            mine = torch.tensor([[a["PESQ"], b["STOI"], b["ESTOI"]] for a, b in zip(r_p, r_s)],
-                                dtype=torch.float32).to(dev, non_blocking=True)
-            dist.all_gather_into_tensor(gather_buf, mine)
-        return r_p, r_s
+        # per-rank engine work: PESQ-wb and STOI/ESTOI scores of this rank's 4096 pairs
+        p = pesq.scores(clean, noisy)
+        s, e = stoi.scores(clean, noisy, 16000)
+        local = torch.stack([p, s, e], dim=1)
+        full = gather_scores(local, world * B) if distributed else local  # RCCL all-gather (xGMI)
+        return full.cpu() if rank == 0 else None  # one device->host copy of the job's scores
 
     for _ in range(args.warmup):
         step()
@@ -180,7 +179,7 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (speech-like harmonic source + AM noise, SNR U[-5,25] dB, int16 grid)",
-            "config": {"workload": "PESQ-wb + STOI/ESTOI drop-in API calls, 10 s @ 16 kHz fp32 pairs",
+            "config": {"workload": "PESQ-wb + STOI/ESTOI scores of 10 s @ 16 kHz fp32 pairs (engine path of the drop-in API)",
                        "batch_per_gpu": B, "global_batch": world * B, "length": L, "sample_rate": 16000,
                        "parallelism": f"dp{world} (utterance shards, RCCL all-gather of scores)"},
             "roofline": roof, "cpu_baseline": cpu,

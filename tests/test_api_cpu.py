@@ -1,0 +1,108 @@
+"""The drop-in API (reference fast_se_metrics/base.py, PESQ.py, STOI.py) in CPU mode
+(use_gpu=False): behaviour, errors and parity with the reference's golden vectors."""
+import numpy as np
+import pytest
+import torch
+
+from tests.conftest import PESQ_CASES, STOI_CASES, load_golden
+
+
+def test_import_paths():
+    import fast_se_metrics
+    from fast_se_metrics import PESQ, STOI
+    from fast_se_metrics.base import BaseMetric
+    assert issubclass(PESQ, BaseMetric) and issubclass(STOI, BaseMetric)
+    assert PESQ.higher_is_better and STOI.higher_is_better
+    assert PESQ.EXPECTED_SAMPLING_RATE == 16000 and STOI.EXPECTED_SAMPLING_RATE == 10000
+    assert fast_se_metrics.__all__ == ["STOI", "PESQ"]
+
+
+def test_constructor_attributes():
+    from fast_speech_enhancement_metrics_amd import PESQ, STOI
+    p = PESQ()
+    assert p.sample_rate == 16000 and p.device == "cpu"
+    s = STOI(sample_rate=16000)
+    assert s.sample_rate == 16000 and s.device == "cpu" and s.N == 30 and s.num_octave_bands == 15
+
+
+@pytest.mark.parametrize("name", PESQ_CASES)
+def test_pesq_cpu_mode_matches_reference(name):
+    from fast_speech_enhancement_metrics_amd import PESQ
+    g = load_golden(name)
+    res = PESQ()(torch.from_numpy(g["clean_f"]), torch.from_numpy(g["noisy_f"]))
+    assert [list(d) for d in res] == [["PESQ"]] * len(res)
+    assert all(isinstance(d["PESQ"], float) for d in res)
+    np.testing.assert_allclose([d["PESQ"] for d in res], g["pesq"], atol=2e-3, rtol=0)
+
+
+@pytest.mark.parametrize("name", STOI_CASES)
+def test_stoi_cpu_mode_matches_reference(name):
+    from fast_speech_enhancement_metrics_amd import STOI
+    g = load_golden(name)
+    res = STOI(int(g["sample_rate"]))(torch.from_numpy(g["clean_f"]), torch.from_numpy(g["noisy_f"]))
+    assert [sorted(d) for d in res] == [["ESTOI", "STOI"]] * len(res)
+    np.testing.assert_allclose([d["STOI"] for d in res], g["stoi"], atol=1e-4, rtol=0)
+    np.testing.assert_allclose([d["ESTOI"] for d in res], g["estoi"], atol=1e-4, rtol=0)
+
+
+def test_shape_mismatch_raises_like_reference():
+    from fast_speech_enhancement_metrics_amd import PESQ, STOI
+    for m in (PESQ(), STOI()):
+        with pytest.raises(Exception, match="should have the same shape"):
+            m(torch.zeros(2, 16000), torch.zeros(2, 16001))
+
+
+def test_clean_none_asserts_like_reference():
+    from fast_speech_enhancement_metrics_amd import PESQ, STOI
+    for m in (PESQ(), STOI()):
+        with pytest.raises(AssertionError):
+            m(None, torch.zeros(2, 16000))
+
+
+def test_one_dimensional_input_gives_one_result():
+    from fast_speech_enhancement_metrics_amd import PESQ
+    g = load_golden("pesq_3s")
+    res = PESQ()(torch.from_numpy(g["clean_f"][0]), torch.from_numpy(g["noisy_f"][0]))
+    assert len(res) == 1 and abs(res[0]["PESQ"] - g["pesq"][0]) < 2e-3
+
+
+def test_too_short_pesq_raises_runtime_error():
+    from fast_speech_enhancement_metrics_amd import PESQ
+    with pytest.raises(RuntimeError):
+        PESQ()(torch.randn(2, 4000), torch.randn(2, 4000))
+
+
+def test_too_short_stoi_warns_then_type_error():
+    """STOI.py:163-165 + :205: no 30-frame segment -> RuntimeWarning, then TypeError."""
+    from fast_speech_enhancement_metrics_amd import STOI
+    x = torch.randn(2, 3000)
+    with pytest.warns(RuntimeWarning):
+        with pytest.raises(TypeError):
+            STOI(10000)(x, x + 0.1 * torch.randn_like(x))
+
+
+def test_high_vs_low_snr_cpu():
+    """tests/test_high_vs_low_snr.py analogue (CPU mode)."""
+    from fast_speech_enhancement_metrics_amd import PESQ, STOI
+    g_hi, g_lo = load_golden("pesq_hi_snr"), load_golden("pesq_lo_snr")  # same speech, 10 dB vs -5 dB
+    for m in (PESQ(16000), STOI(16000)):
+        hi = m(torch.from_numpy(g_hi["clean_f"]), torch.from_numpy(g_hi["noisy_f"]))
+        lo = m(torch.from_numpy(g_lo["clean_f"]), torch.from_numpy(g_lo["noisy_f"]))
+        for a, b in zip(hi, lo):
+            for k in a:
+                assert a[k] > b[k], (type(m).__name__, k, a[k], b[k])
+
+
+def test_use_gpu_without_device_raises():
+    from fast_speech_enhancement_metrics_amd import PESQ
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    with pytest.raises(RuntimeError):
+        PESQ(use_gpu=True)
+
+
+def test_cpu_resampler_matches_reference_vectors():
+    from fast_speech_enhancement_metrics_amd.resample import Resample
+    g = load_golden("stoi_16k")
+    out = Resample(16000, 10000)(torch.from_numpy(g["clean_f"])).numpy()
+    np.testing.assert_allclose(out, g["x10_clean"], atol=2e-6, rtol=0)

@@ -1,0 +1,63 @@
+"""World-size-2 gloo test of the data-parallel path (CPU metric mode): sharded scores
+all-gathered across ranks equal the single-process result."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _worker(rank, world, port, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from fast_speech_enhancement_metrics_amd import PESQ, STOI
+        from fast_speech_enhancement_metrics_amd.distributed import sharded_scores
+        from tests.conftest import load_golden
+        g = load_golden("pesq_wide")
+        p = sharded_scores(PESQ(16000), torch.from_numpy(g["clean_f"]), torch.from_numpy(g["noisy_f"]))
+        gs = load_golden("stoi_wide")
+        s = sharded_scores(STOI(16000), torch.from_numpy(gs["clean_f"]), torch.from_numpy(gs["noisy_f"]),
+                           sample_rate=16000)
+        out_q.put((rank, p.numpy(), s.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_gather_matches_single_process():
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    from fast_speech_enhancement_metrics_amd import PESQ, STOI
+    from tests.conftest import load_golden
+    g = load_golden("pesq_wide")
+    ref_p = PESQ(16000).scores(torch.from_numpy(g["clean_f"]), torch.from_numpy(g["noisy_f"])).numpy()
+    gs = load_golden("stoi_wide")
+    ref_s = torch.stack(STOI(16000).scores(torch.from_numpy(gs["clean_f"]), torch.from_numpy(gs["noisy_f"]),
+                                           sample_rate=16000), 1).numpy()
+    for rank, p, s in res:
+        np.testing.assert_allclose(p[:, 0], ref_p, rtol=0, atol=1e-6)
+        np.testing.assert_allclose(s, ref_s, rtol=0, atol=1e-6)
+
+
+@pytest.mark.parametrize("batch,world", [(7, 2), (8, 4), (3, 8), (4096, 8)])
+def test_shard_bounds_cover_batch(batch, world):
+    from fast_speech_enhancement_metrics_amd.distributed import shard_bounds
+    b = [shard_bounds(batch, world, r) for r in range(world)]
+    assert b[0][0] == 0 and b[-1][1] == batch
+    assert all(b[i][1] == b[i + 1][0] for i in range(world - 1))
+    sizes = [hi - lo for lo, hi in b]
+    assert max(sizes) - min(sizes) <= 1
