@@ -120,7 +120,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    distributed = world > 1
+    distributed = "WORLD_SIZE" in os.environ  # launched by torch.distributed.run (any N)
     if distributed:
         import torch.distributed as dist
         torch.cuda.set_device(local)

@@ -14,6 +14,15 @@
 
 namespace fsem {
 
+// Workgroup barrier that orders LDS only.  __syncthreads() also waits for every outstanding
+// global load/store (vmcnt(0)), which would drain the next tile's prefetch at every barrier;
+// kernels that communicate through LDS alone use this instead.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
@@ -36,9 +45,9 @@ __device__ __forceinline__ float wave_max(float v) {
 __device__ __forceinline__ float block_sum_256(float v, float *scratch) {
   v = wave_sum(v);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  __syncthreads();
+  lds_barrier();
   if (lane == 0) scratch[w] = v;
-  __syncthreads();
+  lds_barrier();
   return scratch[0] + scratch[1] + scratch[2] + scratch[3];
 }
 

@@ -52,10 +52,10 @@ __device__ unsigned long long g_stamps[kStampBlocks][16];
 #endif
 
 constexpr int PT = 256;
-constexpr int CH = FSEM_PESQ_CH;  // 60 samples per lane
+constexpr int CH = FSEM_PESQ_CH;  // 52 samples per lane (stride 208 B: conflict-free b128)
 constexpr int TILE = PT * CH;     // 15360
 constexpr int WARM = 768;
-constexpr int NF = 56;            // frames per segment
+constexpr int NF = 48;            // frames per segment
 constexpr int OWN = NF * 256;     // samples of band-pass power owned per segment
 constexpr int NBARK = 49;
 constexpr int NS = 12;            // scan states: 10 band-pass (5 sections) + 2 pre-emphasis
@@ -140,7 +140,7 @@ __device__ __forceinline__ void iir_pass1(const float4 *__restrict__ my4, int64_
 
 // IIR pass 2 from the true start state z: band-pass cascade (power over owned samples) and
 // pre-emphasis, whose output overwrites the chunk in place (zero from `lim` on).
-template <bool TAPER>
+template <bool TAPER, bool MASK>
 __device__ __forceinline__ float iir_pass2(float4 *__restrict__ w4, float z[NS], int own_lo, int own_hi,
                                            int lim, int64_t t_lane, int64_t L) {
   const float b0 = kPreB[0], b1 = kPreB[1], b2 = kPreB[2], a1 = kPreA[1], a2 = kPreA[2];
@@ -161,12 +161,12 @@ __device__ __forceinline__ float iir_pass2(float4 *__restrict__ w4, float z[NS],
         z[2 * k + 1] = fmaf(-kBpSecA[k][1], y, -u);
         u = y;
       }
-      acc = (n >= own_lo && n < own_hi) ? fmaf(u, u, acc) : acc;
+      acc = (!MASK || (n >= own_lo && n < own_hi)) ? fmaf(u, u, acc) : acc;
       const float xp = TAPER ? xs[c] * taper_w(tf0 + (float)n, Lf) : xs[c];
       const float y = fmaf(b0, xp, z[NBP]);
       z[NBP] = fmaf(b1, xp, fmaf(-a1, y, z[NBP + 1]));
       z[NBP + 1] = fmaf(b2, xp, -a2 * y);
-      xs[c] = (n < lim) ? y : 0.f;  // the reference zero-pads AFTER the filter (PESQ.py:128)
+      xs[c] = (!MASK || n < lim) ? y : 0.f;  // the reference zero-pads AFTER the filter (PESQ.py:128)
     }
     w4[q] = make_float4(xs[0], xs[1], xs[2], xs[3]);
   }
@@ -215,7 +215,7 @@ __global__ void __launch_bounds__(PT, 2)
 #pragma unroll
       for (int k = 0; k < PF; ++k) t4[tid + PT * k] = pre[k];
     }
-    __syncthreads();
+    lds_barrier();
     STAMP(1);
     const int g = it.g;
     const int64_t tstart = it.tstart;
@@ -237,7 +237,7 @@ __global__ void __launch_bounds__(PT, 2)
     float *const mine = xbuf + tid * SCAN_LD;
 #pragma unroll
     for (int i = 0; i < NS; ++i) mine[i] = e[i];
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int lv = 0; lv < 4; ++lv) {
       const int d = 1 << lv;
@@ -246,7 +246,7 @@ __global__ void __launch_bounds__(PT, 2)
       const float keep = (tid >= d) ? 1.f : 0.f;
 #pragma unroll
       for (int i = 0; i < NS; ++i) q[i] = src[i] * keep;
-      __syncthreads();
+      lds_barrier();
 #pragma unroll
       for (int i = 0; i < NBP; ++i) {
         float acc = e[i];
@@ -264,13 +264,13 @@ __global__ void __launch_bounds__(PT, 2)
       if (lv < 3) {
 #pragma unroll
         for (int i = 0; i < NS; ++i) mine[i] = e[i];
-        __syncthreads();
+        lds_barrier();
       }
     }
     // start state of chunk j = inclusive prefix of chunk j-1
 #pragma unroll
     for (int i = 0; i < NS; ++i) mine[i] = e[i];
-    __syncthreads();
+    lds_barrier();
     float z[NS];
     {
       const float *src = xbuf + max(tid - 1, 0) * SCAN_LD;
@@ -282,19 +282,21 @@ __global__ void __launch_bounds__(PT, 2)
 
     // ---------------------------------------------------------------- IIR pass 2
     {
-      const int64_t own_len = (g < npseg) ? min((int64_t)OWN, L - (int64_t)g * OWN) : 0;
+      const int64_t own_len = (g == nseg - 1) ? L - (int64_t)g * OWN : min((int64_t)OWN, L - (int64_t)g * OWN);
       const int own_lo = WARM - CH * tid, own_hi = WARM + (int)own_len - CH * tid;  // chunk-local
       const int lim = (int)min((int64_t)CH, max((int64_t)0, L - t_lane));       // y = 0 from here
       float4 *w4 = reinterpret_cast<float4 *>(tile + CH * tid);
       float acc;
+      // masks are only needed where a wave's chunks straddle the owned range or L
+      const bool plain = own_lo <= 0 && own_hi >= CH && lim >= CH;
       if (__builtin_amdgcn_readfirstlane((int)wave_edge))
-        acc = iir_pass2<true>(w4, z, own_lo, own_hi, lim, t_lane, L);
+        acc = iir_pass2<true, true>(w4, z, own_lo, own_hi, lim, t_lane, L);
       else
-        acc = iir_pass2<false>(w4, z, own_lo, own_hi, lim, t_lane, L);
+        acc = iir_pass2<false, true>(w4, z, own_lo, own_hi, lim, t_lane, L);
       const float tot = block_sum_256(acc, red);
       if (tid == 0) ppart[it.s * nseg + g] = tot * (kBpGain * kBpGain);
     }
-    __syncthreads();
+    lds_barrier();
     STAMP(4);
     // issue the next item's tile loads now: they stay in flight through the FFT / Bark
     // phases (the IIR phases above run without the prefetch registers live)
@@ -337,7 +339,7 @@ __global__ void __launch_bounds__(PT, 2)
           pb[0] = 0.f;
         }
       }
-      __syncthreads();  // every wave is done reading the tile for this round
+      lds_barrier();  // every wave is done reading the tile for this round
       STAMP(6 + rd);
       if (active) {  // park the spectra in the consumed part of the tile
         float *ra = tile + SPEC_LD * fa;
@@ -349,7 +351,7 @@ __global__ void __launch_bounds__(PT, 2)
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
     STAMP(13);
 
     // ---------------------------------------------------------------- Bark bands on MFMA
@@ -369,27 +371,54 @@ __global__ void __launch_bounds__(PT, 2)
         bcor[t] = bcor_c[t];
         asm volatile("" : "+v"(blo[t]), "+v"(bhi[t]), "+v"(bcor[t]));
       }
-      for (int kk = kBarkTileK[0][0]; kk < kBarkTileK[0][1]; ++kk) {
-        const int bin = 4 * kk + kq;
-        c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(srow[bin], (bin >= blo[0] && bin < bhi[0]) ? bcor[0] : 0.f, c0, 0, 0, 0);
-      }
-      for (int kk = kBarkTileK[1][0]; kk < kBarkTileK[1][1]; ++kk) {
-        const int bin = 4 * kk + kq;
-        c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(srow[bin], (bin >= blo[1] && bin < bhi[1]) ? bcor[1] : 0.f, c1, 0, 0, 0);
-      }
-      for (int kk = kBarkTileK[2][0]; kk < kBarkTileK[2][1]; kk += 2) {
-        const int bin = 4 * kk + kq;
-        c2a = __builtin_amdgcn_mfma_f32_16x16x4f32(srow[bin], (bin >= blo[2] && bin < bhi[2]) ? bcor[2] : 0.f, c2a, 0, 0, 0);
-        if (kk + 1 < kBarkTileK[2][1]) {
-          const int bin2 = bin + 4;
-          c2b = __builtin_amdgcn_mfma_f32_16x16x4f32(srow[bin2], (bin2 >= blo[2] && bin2 < bhi[2]) ? bcor[2] : 0.f, c2b, 0, 0, 0);
+      // A operand: the wave's 16 spectrum rows, one bin per lane per K-step; issue all LDS
+      // reads of a tile before its MFMA chain (the chain then never waits on LDS latency)
+      constexpr int K0a = kBarkTileK[0][0], K0b = kBarkTileK[0][1];
+      constexpr int K1a = kBarkTileK[1][0], K1b = kBarkTileK[1][1];
+      constexpr int K2a = kBarkTileK[2][0], K2b = kBarkTileK[2][1];
+      constexpr int K3a = kBarkTileK[3][0], K3b = kBarkTileK[3][1];
+      {
+        float a0[K0b - K0a], a1[K1b - K1a], a3[K3b - K3a];
+#pragma unroll
+        for (int k = 0; k < K0b - K0a; ++k) a0[k] = srow[4 * (K0a + k) + kq];
+#pragma unroll
+        for (int k = 0; k < K1b - K1a; ++k) a1[k] = srow[4 * (K1a + k) + kq];
+#pragma unroll
+        for (int k = 0; k < K3b - K3a; ++k) a3[k] = srow[4 * (K3a + k) + kq];
+#pragma unroll
+        for (int k = 0; k < K0b - K0a; ++k) {
+          const int bin = 4 * (K0a + k) + kq;
+          c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[k], (bin >= blo[0] && bin < bhi[0]) ? bcor[0] : 0.f, c0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int k = 0; k < K1b - K1a; ++k) {
+          const int bin = 4 * (K1a + k) + kq;
+          c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[k], (bin >= blo[1] && bin < bhi[1]) ? bcor[1] : 0.f, c1, 0, 0, 0);
+        }
+#pragma unroll
+        for (int k = 0; k < K3b - K3a; ++k) {
+          const int bin = 4 * (K3a + k) + kq;
+          c3 = __builtin_amdgcn_mfma_f32_16x16x4f32(a3[k], (bin >= blo[3] && bin < bhi[3]) ? bcor[3] : 0.f, c3, 0, 0, 0);
         }
       }
-      for (int kk = kBarkTileK[3][0]; kk < kBarkTileK[3][1]; ++kk) {
-        const int bin = 4 * kk + kq;
-        c3 = __builtin_amdgcn_mfma_f32_16x16x4f32(srow[bin], (bin >= blo[3] && bin < bhi[3]) ? bcor[3] : 0.f, c3, 0, 0, 0);
+      constexpr int KB = 16;  // tile 2 in batches of 16 K-steps, two accumulators
+#pragma unroll
+      for (int k0 = K2a; k0 < K2b; k0 += KB) {
+        float a2[KB];
+#pragma unroll
+        for (int k = 0; k < KB; ++k) a2[k] = (k0 + k < K2b) ? srow[4 * (k0 + k) + kq] : 0.f;
+#pragma unroll
+        for (int k = 0; k < KB; ++k) {
+          if (k0 + k < K2b) {
+            const int bin = 4 * (k0 + k) + kq;
+            const float bv = (bin >= blo[2] && bin < bhi[2]) ? bcor[2] : 0.f;
+            if (k & 1)
+              c2b = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[k], bv, c2b, 0, 0, 0);
+            else
+              c2a = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[k], bv, c2a, 0, 0, 0);
+          }
+        }
       }
-      // C/D: col = lane & 15 (band in tile), row = 4 * (lane >> 4) + i (frame in group)
       float *brow = bark + ((int64_t)it.s * F + (int64_t)g * NF + 16 * wave) * NBARK;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -403,7 +432,7 @@ __global__ void __launch_bounds__(PT, 2)
         }
       }
     }
-    __syncthreads();  // tile is rewritten by the next item
+    lds_barrier();  // tile is rewritten by the next item
     STAMP(15);
   }
 }
@@ -600,11 +629,14 @@ struct Geometry {
   int F, nfseg, npseg, nseg;
 };
 
+// Segment g owns band-pass power samples [g*OWN, (g+1)*OWN); the LAST segment owns
+// [g*OWN, L), which its tile must cover: L - (nseg-1)*OWN <= TILE - WARM.
 inline Geometry geometry(int64_t L) {
   Geometry g;
   g.F = frames_of(L);
   g.nfseg = (g.F + NF - 1) / NF;
-  g.npseg = (int)((L + OWN - 1) / OWN);
+  const int64_t span = TILE - WARM;
+  g.npseg = L <= span ? 1 : (int)((L - span + OWN - 1) / OWN) + 1;
   g.nseg = g.nfseg > g.npseg ? g.nfseg : g.npseg;
   return g;
 }

@@ -57,7 +57,7 @@ __global__ void __launch_bounds__(256, 2)
     stoi_resample_vad16(const float *__restrict__ ref, const float *__restrict__ deg, int64_t n_in, int64_t ld,
                         int64_t L10, int NV, int nchunk, int64_t nitems, float *__restrict__ y10, int64_t y_ld,
                         float *__restrict__ energy, int nv_ld) {
-  __shared__ __attribute__((aligned(16))) float xin[XPF * 256 * 4];
+  __shared__ __attribute__((aligned(16))) float xin[XPF * 256 * 4 + 4];
   __shared__ __attribute__((aligned(16))) float ytile[YT + 8];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t nbytes = (uint32_t)(((n_in + 3) & ~(int64_t)3) * 4);
@@ -67,7 +67,7 @@ __global__ void __launch_bounds__(256, 2)
     b = bc / nchunk;
     chunk = (int)(bc - b * nchunk);
     o0 = (int64_t)chunk * (VF2 * 128);
-    i0 = 8 * (o0 / 5) - 12;  // 4-aligned base; group m reads x[8m - 10 + t] = xin[8(m - m0) + 2 + t]
+    i0 = 8 * (o0 / 5) - 12;  // 4-aligned base; group m reads x[8m - 10 + t] = xin[8(m - m0) + 4 + t]
   };
   auto prefetch = [&](int64_t item, float4 pre[XPF]) {
     int64_t b, o0, i0;
@@ -102,22 +102,28 @@ __global__ void __launch_bounds__(256, 2)
     int64_t b, o0, i0;
     int chunk, sig;
     item_src(item, b, chunk, sig, o0, i0);
-    float4 *x4 = reinterpret_cast<float4 *>(xin);
+    // staged at +2 floats: group m's 28 taps then start 16-byte aligned at xin[8(m - m0) + 4]
+    float2 *x2 = reinterpret_cast<float2 *>(xin + 2);
 #pragma unroll
-    for (int k = 0; k < XPF; ++k) x4[tid + 256 * k] = pre[k];
-    __syncthreads();
+    for (int k = 0; k < XPF; ++k) {
+      x2[2 * (tid + 256 * k)] = make_float2(pre[k].x, pre[k].y);
+      x2[2 * (tid + 256 * k) + 1] = make_float2(pre[k].z, pre[k].w);
+    }
+    lds_barrier();
     if (item + gridDim.x < nitems) prefetch(item + gridDim.x, pre);
     const int64_t o_end = min(o0 + (int64_t)YT, L10);
     const int64_t m0 = o0 / 5;
     const int64_t m1 = (o_end + 4) / 5;
     for (int64_t m = m0 + tid; m < m1; m += 256) {
-      const float2 *xs2 = reinterpret_cast<const float2 *>(xin + 8 * (m - m0) + 2);
+      const float4 *xs4 = reinterpret_cast<const float4 *>(xin + 8 * (m - m0) + 4);
       float v[28];
 #pragma unroll
-      for (int t = 0; t < 14; ++t) {
-        const float2 q = xs2[t];
-        v[2 * t] = q.x;
-        v[2 * t + 1] = q.y;
+      for (int t = 0; t < 7; ++t) {
+        const float4 q = xs4[t];
+        v[4 * t] = q.x;
+        v[4 * t + 1] = q.y;
+        v[4 * t + 2] = q.z;
+        v[4 * t + 3] = q.w;
       }
 #pragma unroll
       for (int j = 0; j < 5; ++j) {
@@ -128,7 +134,7 @@ __global__ void __launch_bounds__(256, 2)
         if (o >= o0 && o < o_end) ytile[o - o0] = acc;
       }
     }
-    __syncthreads();
+    lds_barrier();
     // store this chunk's own 10 kHz samples (float4, coalesced; y_ld % 64 == 0, o0 % 4 == 0)
     const int nown = (int)min((int64_t)(VF2 * 128), L10 - o0);
     float *__restrict__ yr = y10 + (b * 2 + sig) * y_ld + o0;
@@ -155,7 +161,7 @@ __global__ void __launch_bounds__(256, 2)
         if (lane == 0) energy[b * nv_ld + i] = 20.f * log10f(sqrtf(acc) + 1e-9f);
       }
     }
-    __syncthreads();
+    lds_barrier();
   }
 }
 
@@ -176,7 +182,7 @@ __global__ void __launch_bounds__(256)
   for (int sig = 0; sig < 2; ++sig) {
     const Src src{(sig == 0 ? ref : deg) + b * ld, n_in};
     for (int k = tid; k < ny; k += 256) ytile[k] = sample10(src, o0 + k, L10, mode == 1, rk);
-    __syncthreads();
+    lds_barrier();
     float *__restrict__ yr = y10 + (b * 2 + sig) * y_ld + o0;
     for (int k = tid; k < nw_own; k += 256) yr[k] = ytile[k];
     if (sig == 0) {
@@ -194,7 +200,7 @@ __global__ void __launch_bounds__(256)
         if (lane == 0) energy[b * nv_ld + i] = 20.f * log10f(sqrtf(acc) + 1e-9f);
       }
     }
-    __syncthreads();
+    lds_barrier();
   }
 }
 
@@ -217,12 +223,12 @@ __global__ void __launch_bounds__(256)
     const unsigned long long bal = __ballot(keep);
     const int pre = __popcll(bal & ((1ull << lane) - 1ull));
     if (lane == 0) wcount[wave] = __popcll(bal);
-    __syncthreads();
+    lds_barrier();
     int off = base;
     for (int w = 0; w < wave; ++w) off += wcount[w];
     if (keep) idx[b * nv_ld + off + pre] = i;
     base += wcount[0] + wcount[1] + wcount[2] + wcount[3];
-    __syncthreads();
+    lds_barrier();
   }
   if (tid == 0) kept[b] = base;
 }
@@ -275,7 +281,7 @@ __global__ void __launch_bounds__(256)
     blk[1][j][lane] = d0;
     blk[1][j][lane + 64] = d1;
   }
-  __syncthreads();
+  lds_barrier();
 
   cf tw1[8], tw2[8];
   fft512_twiddles(lane, tw1, tw2);
@@ -283,6 +289,10 @@ __global__ void __launch_bounds__(256)
   float2 *wbuf = reinterpret_cast<float2 *>(xbuf) + wave * kFftBuf;
   float *pbuf = reinterpret_cast<float *>(wbuf);
   const int plane = (64 - lane) & 63;
+  const int pc_sig = kObmPiece[lane][0], pc_band = kObmPiece[lane][1];
+  const int pc_lo = kObmPiece[lane][2], pc_hi = kObmPiece[lane][3];
+  const int pc_end = kObmPiece[lane][4];
+  const bool pc_head = kObmPiece[lane][5] != 0;
   for (int k = k0 + wave; k < kend; k += 4) {
     const int j = k - k0;  // frame k = [block_{k+1}, block_{k+2}] * w
     cf v[8];
@@ -313,12 +323,18 @@ __global__ void __launch_bounds__(256)
       pbuf[256 + lane + 64 * r] = pd[r];
     }
     wave_lds_fence();
-    if (lane < 2 * NB) {
-      const int sig = lane / NB, band = lane - sig * NB;
-      const float *ps = pbuf + 256 * sig;
+    {
+      // band sums: one <=9-bin piece per lane, segmented shuffle reduction per band
+      const float *ps = pbuf + 256 * pc_sig;
       float acc = 0.f;
-      for (int bin = kObmEdge[band][0]; bin < kObmEdge[band][1]; ++bin) acc += ps[bin];
-      tob[((b + sig * B) * NB + band) * tmax + k] = sqrtf(acc);
+#pragma unroll
+      for (int i = 0; i < 9; ++i) acc += (pc_lo + i < pc_hi) ? ps[pc_lo + i] : 0.f;
+#pragma unroll
+      for (int off = 1; off < 8; off <<= 1) {
+        const float v = __shfl_down(acc, off, 64);
+        if (lane + off < pc_end) acc += v;
+      }
+      if (pc_head) tob[((b + pc_sig * B) * NB + pc_band) * tmax + k] = sqrtf(acc);
     }
     wave_lds_fence();
   }
@@ -352,14 +368,14 @@ __global__ void __launch_bounds__(SEG_T)
   const float *xd = tob + ((b + B) * NB) * tmax;
   double st = 0.0, et = 0.0;
   for (int m0 = 0; m0 < S; m0 += SEG_T) {
-    __syncthreads();
+    lds_barrier();
     const int nf = min(W, T - m0);
     for (int e = tid; e < NB * W; e += SEG_T) {
       const int j = e / W, t = e - j * W;
       X[j][t] = (t < nf) ? xc[j * tmax + m0 + t] : 0.f;
       Y[j][t] = (t < nf) ? xd[j * tmax + m0 + t] : 0.f;
     }
-    __syncthreads();
+    lds_barrier();
     const int m = m0 + tid;
     if (m < S) {
       float s_acc = 0.f;
@@ -439,12 +455,12 @@ __global__ void __launch_bounds__(SEG_T)
   // deterministic 2-wave reduction
   st = wave_sum_d(st);
   et = wave_sum_d(et);
-  __syncthreads();
+  lds_barrier();
   if ((tid & 63) == 0) {
     red[(tid >> 6) * 2] = st;
     red[(tid >> 6) * 2 + 1] = et;
   }
-  __syncthreads();
+  lds_barrier();
   if (tid == 0) {
     stoi_out[b] = (float)((red[0] + red[2]) / NB / S);   // compute_correlation / num_segments (STOI.py:150,198)
     estoi_out[b] = (float)((red[1] + red[3]) / NSEG / S);
