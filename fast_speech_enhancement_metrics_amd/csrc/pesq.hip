@@ -116,10 +116,15 @@ __device__ __forceinline__ void prefetch(const Item &it, int64_t L, int tid, flo
 
 // IIR pass 1: end states of this lane's chunk from zero state -- band-pass (states 0..9,
 // untapered input) and pre-emphasis (states 10..11, tapered input).  Fully unrolled: the
-// kBpG / kPreG functionals become literal-operand FMAs.
+// functionals (kScanG, __constant__) come in by scalar loads as SGPR operands.
 template <bool TAPER>
 __device__ __forceinline__ void iir_pass1(const float4 *__restrict__ my4, int64_t t_lane, int64_t L, float e[NS]) {
   const float tf0 = (float)t_lane, Lf = (float)L;
+  // opaque table pointer: the rows stay memory operands (s_load) instead of folded literals
+  uint64_t gaddr = reinterpret_cast<uint64_t>(&kScanG[0][0]);
+  asm volatile("" : "+s"(gaddr));
+  typedef const __attribute__((address_space(4))) float crow[NS];
+  crow *G = reinterpret_cast<crow *>(gaddr);
 #pragma unroll
   for (int i = 0; i < NS; ++i) e[i] = 0.f;
 #pragma unroll
@@ -130,10 +135,10 @@ __device__ __forceinline__ void iir_pass1(const float4 *__restrict__ my4, int64_
     for (int c = 0; c < 4; ++c) {
       const int n = 4 * q + c;
 #pragma unroll
-      for (int i = 0; i < NBP; ++i) e[i] = fmaf(kBpG[n][i], xs[c], e[i]);
+      for (int i = 0; i < NBP; ++i) e[i] = fmaf(G[n][i], xs[c], e[i]);
       const float xp = TAPER ? xs[c] * taper_w(tf0 + (float)n, Lf) : xs[c];
-      e[NBP] = fmaf(kPreG[n][0], xp, e[NBP]);
-      e[NBP + 1] = fmaf(kPreG[n][1], xp, e[NBP + 1]);
+      e[NBP] = fmaf(G[n][NBP], xp, e[NBP]);
+      e[NBP + 1] = fmaf(G[n][NBP + 1], xp, e[NBP + 1]);
     }
   }
 }
