@@ -96,7 +96,7 @@ def kernel_roofline(pesq, clean, noisy, reps):
     h = stream.cuda_stream
 
     def launch():
-        _native.check(lib.fsem_pesq_front_f32(clean.data_ptr(), noisy.data_ptr(), B, L, L, bark.data_ptr(),
+        _native.check(lib.fsem_pesq_front_f32(clean.data_ptr(), noisy.data_ptr(), B, L, L, None, bark.data_ptr(),
                                               power.data_ptr(), ws.data_ptr(), ws.numel(), h), "front")
 
     launch()

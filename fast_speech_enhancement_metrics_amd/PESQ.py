@@ -10,7 +10,7 @@ from __future__ import annotations
 import torch
 
 from . import _cpu, _native
-from .base import BaseMetric, as_rows
+from .base import BaseMetric, as_rows, device_lengths
 
 
 class PESQ(BaseMetric):
@@ -21,8 +21,12 @@ class PESQ(BaseMetric):
         super().__init__(sample_rate, use_gpu)
 
     # ------------------------------------------------------------------ device paths
-    def scores(self, clean_speech: torch.Tensor, denoised_speech: torch.Tensor) -> torch.Tensor:
-        """Per-utterance MOS as a tensor on the metric's device (no host sync on GPU)."""
+    def scores(self, clean_speech: torch.Tensor, denoised_speech: torch.Tensor, lengths=None) -> torch.Tensor:
+        """Per-utterance MOS as a tensor on the metric's device (no host sync on GPU).
+
+        16 kHz rows.  ``lengths`` (optional, [B] ints): row b holds lengths[b] samples and scores
+        as the reference would on that unpadded row alone; rows under 20 frames give NaN.
+        """
         clean = as_rows(clean_speech)
         noisy = as_rows(denoised_speech)
         B, L = clean.shape
@@ -30,9 +34,12 @@ class PESQ(BaseMetric):
             raise Exception("`clean_speech` and `denoised_speech` should have the same shape.")
         lib = _native.load() if clean.is_cuda else None
         if lib is None:
-            return _cpu.pesq(clean, noisy)
+            if lengths is None:
+                return _cpu.pesq(clean, noisy)
+            return _cpu.per_row(_cpu.pesq, clean, noisy, device_lengths(lengths, B, L, "cpu"))
         F = lib.fsem_pesq_frames(L)
-        if F < 20:
+        lens = device_lengths(lengths, B, L, clean.device) if lengths is not None else None
+        if F < 20 and lens is None:
             # the reference's unfold(1, size=20, step=10) fails here (PESQ.py:169)
             raise RuntimeError(f"maximum size for tensor at dimension 1 is {max(F, 0)} but size is 20")
         if clean.stride(0) != noisy.stride(0) or L % 4:
@@ -43,12 +50,14 @@ class PESQ(BaseMetric):
         mos = torch.empty(B, dtype=torch.float32, device=clean.device)
         ws = _native.workspace(lib.fsem_pesq_workspace_bytes(B, L), clean.device)
         _native.check(lib.fsem_pesq_wb_f32(clean.data_ptr(), noisy.data_ptr(), B, L, clean.stride(0),
+                                           lens.data_ptr() if lens is not None else None,
                                            mos.data_ptr(), ws.data_ptr(), ws.numel(),
                                            _native.stream_handle(clean.device)), "PESQ")
         return mos
 
-    def compute_metric(self, clean_speech: torch.Tensor | None, denoised_speech: torch.Tensor) -> list[dict[str, float]]:
+    def compute_metric(self, clean_speech: torch.Tensor | None, denoised_speech: torch.Tensor,
+                       lengths=None) -> list[dict[str, float]]:
         assert clean_speech is not None
         with torch.inference_mode():
-            mos = self.scores(clean_speech, denoised_speech)
+            mos = self.scores(clean_speech, denoised_speech, lengths)
             return [{"PESQ": m} for m in mos.tolist()]

@@ -12,7 +12,8 @@ import warnings
 import torch
 
 from . import _cpu, _native
-from .base import BaseMetric, as_rows
+from .base import BaseMetric, as_rows, device_lengths, zero_tail
+from .batching import resampled_lengths
 
 
 class STOI(BaseMetric):
@@ -31,8 +32,13 @@ class STOI(BaseMetric):
         self.beta = -15.0
         self.dynamic_range = 40
 
-    def scores(self, clean_speech: torch.Tensor, denoised_speech: torch.Tensor, sample_rate: int | None = None):
-        """(stoi[B], estoi[B]) tensors on the metric's device; NaN where no segment exists."""
+    def scores(self, clean_speech: torch.Tensor, denoised_speech: torch.Tensor, sample_rate: int | None = None,
+               lengths=None):
+        """(stoi[B], estoi[B]) tensors on the metric's device; NaN where no segment exists.
+
+        Rows at ``sample_rate`` (default 10 kHz).  ``lengths`` (optional, [B] ints at that rate):
+        row b holds lengths[b] samples and scores as the reference would on the unpadded row.
+        """
         sr = self.EXPECTED_SAMPLING_RATE if sample_rate is None else int(sample_rate)
         clean = as_rows(clean_speech)
         noisy = as_rows(denoised_speech)
@@ -40,10 +46,17 @@ class STOI(BaseMetric):
             raise Exception("`clean_speech` and `denoised_speech` should have the same shape.")
         B, L = clean.shape
         if not clean.is_cuda:
+            if lengths is not None:
+                lens = device_lengths(lengths, B, L, "cpu")
+                if sr != self.EXPECTED_SAMPLING_RATE:
+                    clean, noisy = self._resample_cpu(zero_tail(clean, lens), sr), self._resample_cpu(zero_tail(noisy, lens), sr)
+                    lens = resampled_lengths(lens, sr, self.EXPECTED_SAMPLING_RATE)
+                return _cpu.per_row(_cpu.stoi, clean, noisy, lens)
             if sr != self.EXPECTED_SAMPLING_RATE:
-                clean, noisy = self.resampler(clean), self.resampler(noisy)
+                clean, noisy = self._resample_cpu(clean, sr), self._resample_cpu(noisy, sr)
             return _cpu.stoi(clean, noisy)
         lib = _native.load()
+        lens = device_lengths(lengths, B, L, clean.device) if lengths is not None else None
         if clean.stride(0) != noisy.stride(0) or L % 4:
             # rows must be readable up to ceil4(L) floats (include/fsem.h): pad odd lengths
             pad = (-L) % 4
@@ -55,7 +68,8 @@ class STOI(BaseMetric):
         if nbytes == 0:
             raise NotImplementedError(f"unsupported sample rate {sr} for the fused STOI resampler")
         ws = _native.workspace(nbytes, clean.device)
-        rc = lib.fsem_stoi_f32(clean.data_ptr(), noisy.data_ptr(), B, L, clean.stride(0), sr, s.data_ptr(),
+        rc = lib.fsem_stoi_f32(clean.data_ptr(), noisy.data_ptr(), B, L, clean.stride(0),
+                               lens.data_ptr() if lens is not None else None, sr, s.data_ptr(),
                                e.data_ptr(), ws.data_ptr(), ws.numel(), _native.stream_handle(clean.device))
         if rc == _native.FSEM_ESHORT:
             raise RuntimeError("STOI input shorter than one 256-sample frame at 10 kHz")
@@ -69,18 +83,26 @@ class STOI(BaseMetric):
             raise TypeError("iteration over a 0-d tensor")
         return [{"STOI": a, "ESTOI": b} for a, b in zip(s, e)]
 
-    def compute_metric(self, clean_speech: torch.Tensor | None, denoised_speech: torch.Tensor) -> list[dict[str, float]]:
+    def _resample_cpu(self, x: torch.Tensor, sr: int) -> torch.Tensor:
+        if sr == self.sample_rate:
+            return self.resampler(x)
+        from .resample import Resample
+        return Resample(sr, self.EXPECTED_SAMPLING_RATE)(x)
+
+    def compute_metric(self, clean_speech: torch.Tensor | None, denoised_speech: torch.Tensor,
+                       lengths=None) -> list[dict[str, float]]:
         assert clean_speech is not None
         with torch.no_grad():
-            return self._finish(*self.scores(clean_speech, denoised_speech))
+            return self._finish(*self.scores(clean_speech, denoised_speech, lengths=lengths))
 
-    def __call__(self, clean_speech: torch.Tensor | None, denoised_speech: torch.Tensor) -> list[dict[str, float]]:
+    def __call__(self, clean_speech, denoised_speech, lengths=None) -> list[dict[str, float]]:
         if self.device == "cuda" and clean_speech is not None:
             # GPU: resampling is fused into the STOI kernels -- skip BaseMetric's resampler
+            clean_speech, denoised_speech, lengths = self.split_ragged(clean_speech, denoised_speech, lengths)
             if clean_speech.shape != denoised_speech.shape:
                 raise Exception("`clean_speech` and `denoised_speech` should have the same shape.")
             clean = torch.atleast_2d(clean_speech).to(self.device)
             noisy = torch.atleast_2d(denoised_speech).to(self.device)
             with torch.no_grad():
-                return self._finish(*self.scores(clean, noisy, self.sample_rate))
-        return super().__call__(clean_speech, denoised_speech)
+                return self._finish(*self.scores(clean, noisy, self.sample_rate, lengths=lengths))
+        return super().__call__(clean_speech, denoised_speech, lengths)

@@ -163,3 +163,23 @@ def stoi(clean: torch.Tensor, noisy: torch.Tensor):
         out_s[b] = (_norm(cx, 2) * _norm(yc, 2)).sum() / 15 / nseg
         out_e[b] = (_norm(_norm(cx, 2), 1) * _norm(_norm(cy, 2), 1)).sum() / 30 / nseg
     return out_s, out_e
+
+
+def per_row(fn, clean: torch.Tensor, noisy: torch.Tensor, lengths: torch.Tensor):
+    """Variable-length CPU mode: ``fn`` on each unpadded row alone (batching.py); rows ``fn``
+    rejects as too short score NaN.  Returns what ``fn`` returns, stacked over rows."""
+    outs = []
+    for b in range(clean.shape[0]):
+        n = int(lengths[b])
+        try:
+            outs.append(fn(clean[b:b + 1, :n], noisy[b:b + 1, :n]))
+        except RuntimeError:
+            outs.append(None)
+    proto = next((o for o in outs if o is not None), None)
+    if proto is None:
+        proto = torch.zeros(1, dtype=torch.float64) if fn is pesq else (torch.zeros(1, dtype=torch.float64),) * 2
+    nan = float("nan")
+    if isinstance(proto, tuple):
+        return tuple(torch.cat([o[i] if o is not None else torch.full((1,), nan, dtype=torch.float64) for o in outs])
+                     for i in range(len(proto)))
+    return torch.cat([o if o is not None else torch.full((1,), nan, dtype=torch.float64) for o in outs])

@@ -39,13 +39,13 @@ SIGNATURES = {
     "fsem_resample_f32": (ctypes.c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _c_i64, _c_i32, _c_i32, _vp]),
     "fsem_pesq_workspace_bytes": (_c_sz, [_c_i64, _c_i64]),
     "fsem_pesq_frames": (ctypes.c_int, [_c_i64]),
-    "fsem_pesq_wb_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_sz, _vp]),
+    "fsem_pesq_wb_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _c_sz, _vp]),
     "fsem_pesq_front_workspace_bytes": (_c_sz, [_c_i64, _c_i64]),
-    "fsem_pesq_front_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _c_sz, _vp]),
+    "fsem_pesq_front_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _c_sz, _vp]),
     "fsem_pesq_back_workspace_bytes": (_c_sz, [_c_i64, _c_i64]),
-    "fsem_pesq_back_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _vp, _vp, _c_sz, _vp]),
+    "fsem_pesq_back_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _vp, _vp, _vp, _c_sz, _vp]),
     "fsem_stoi_workspace_bytes": (_c_sz, [_c_i64, _c_i64, _c_i32]),
-    "fsem_stoi_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _c_i64, _c_i32, _vp, _vp, _vp, _c_sz, _vp]),
+    "fsem_stoi_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _c_i32, _vp, _vp, _vp, _c_sz, _vp]),
     "fsem_stoi_tob_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_i64, _vp, _c_sz, _vp]),
 }
 

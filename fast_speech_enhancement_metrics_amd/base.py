@@ -12,6 +12,7 @@ from abc import ABC, abstractmethod
 import torch
 
 from . import _native
+from .batching import as_lengths, pad_batch, resampled_lengths
 from .resample import Resample
 
 
@@ -45,12 +46,53 @@ class BaseMetric(ABC):
         return clean_speech, denoised_speech
 
     @abstractmethod
-    def compute_metric(self, clean_speech: torch.Tensor | None, denoised_speech: torch.Tensor) -> list[dict[str, float]]:
+    def compute_metric(self, clean_speech: torch.Tensor | None, denoised_speech: torch.Tensor,
+                       lengths: torch.Tensor | None = None) -> list[dict[str, float]]:
         raise NotImplementedError
 
-    def __call__(self, clean_speech: torch.Tensor | None, denoised_speech: torch.Tensor) -> list[dict[str, float]]:
+    def __call__(self, clean_speech, denoised_speech, lengths=None) -> list[dict[str, float]]:
+        """The reference's call (base.py:41-43), extended to ragged batches: lists of 1-D
+        utterances, or padded [B, L] tensors with per-row ``lengths`` (see batching.py)."""
+        clean_speech, denoised_speech, lengths = self.split_ragged(clean_speech, denoised_speech, lengths)
+        if lengths is not None and self.sample_rate != self.EXPECTED_SAMPLING_RATE:
+            # the resampler must see each row zero-padded, as the row alone would be
+            clean_speech = zero_tail(clean_speech, lengths)
+            denoised_speech = zero_tail(denoised_speech, lengths)
         clean_speech, denoised_speech = self.prepare_inputs(clean_speech, denoised_speech)
-        return self.compute_metric(clean_speech, denoised_speech)
+        if lengths is None:
+            return self.compute_metric(clean_speech, denoised_speech)
+        lengths = resampled_lengths(lengths, self.sample_rate, self.EXPECTED_SAMPLING_RATE)
+        return self.compute_metric(clean_speech, denoised_speech, lengths=lengths)
+
+    @staticmethod
+    def split_ragged(clean_speech, denoised_speech, lengths):
+        """-> (clean, denoised, lengths | None) with lengths validated against the row capacity."""
+        if isinstance(denoised_speech, (list, tuple)):
+            if lengths is not None:
+                raise ValueError("pass either lists of utterances or padded tensors with lengths")
+            return pad_batch(clean_speech, denoised_speech)
+        if lengths is not None:
+            d = torch.atleast_2d(denoised_speech)
+            lengths = as_lengths(lengths, d.shape[0], d.shape[-1])
+        return clean_speech, denoised_speech, lengths
+
+
+def zero_tail(x: torch.Tensor | None, lengths: torch.Tensor) -> torch.Tensor | None:
+    """Zero every sample of row b at or past lengths[b]."""
+    if x is None:
+        return None
+    x = torch.atleast_2d(x)
+    t = torch.arange(x.shape[-1], device=x.device)
+    return torch.where(t[None, :] < lengths.to(x.device, torch.int64)[:, None], x, torch.zeros((), dtype=x.dtype,
+                                                                                               device=x.device))
+
+
+def device_lengths(lengths, batch: int, capacity: int, device) -> torch.Tensor:
+    """Validated int32 per-row lengths on `device` (the C-ABI's `lengths` array)."""
+    if isinstance(lengths, torch.Tensor) and lengths.is_cuda and lengths.dtype == torch.int32 \
+            and lengths.numel() == batch:
+        return lengths.contiguous()  # trusted device array: no host round trip
+    return as_lengths(lengths, batch, capacity).to(device)
 
 
 def as_rows(x: torch.Tensor) -> torch.Tensor:

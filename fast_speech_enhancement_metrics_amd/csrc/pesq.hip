@@ -69,6 +69,36 @@ static_assert(PT * SCAN_LD <= XBUF, "scan buffer fits the exchange buffer");
 static_assert(SPEC_LD * (NF - 1) + 256 <= TILE, "parked spectra stay in the tile");
 static_assert(TILE % (4 * PT) == 0, "prefetch split");
 
+__host__ __device__ inline int frames_of(int64_t L) {
+  const int64_t Lp = L + (L % 256);  // PESQ.py:128-130: pad by L % 256 (sic)
+  if (Lp < 512) return 0;
+  return (int)(1 + (Lp - 512) / 256);
+}
+
+struct Geometry {
+  int F, nfseg, npseg, nseg;
+};
+
+// Segment g owns band-pass power samples [g*OWN, (g+1)*OWN); the LAST segment owns
+// [g*OWN, L), which its tile must cover: L - (nseg-1)*OWN <= TILE - WARM.  Every field is
+// non-decreasing in L, so the geometry of the longest row bounds every shorter row's.
+__host__ __device__ inline Geometry geometry(int64_t L) {
+  Geometry g;
+  g.F = frames_of(L);
+  g.nfseg = (g.F + NF - 1) / NF;
+  const int64_t span = TILE - WARM;
+  g.npseg = L <= span ? 1 : (int)((L - span + OWN - 1) / OWN) + 1;
+  g.nseg = g.nfseg > g.npseg ? g.nfseg : g.npseg;
+  return g;
+}
+
+// Row length of utterance b: the per-row length when given (clamped to [0, L]), else L.
+__device__ __forceinline__ int64_t row_length(const int32_t *__restrict__ lens, int64_t b, int64_t L) {
+  if (!lens) return L;
+  const int64_t n = lens[b];
+  return n < 0 ? 0 : (n > L ? L : n);
+}
+
 // PESQ.py:90,108-109: first 15 samples x (t+1)/16, last 15 samples x (L-t)/16, else 1:
 // w(t) = sat((t+1)/16) * sat((L-t)/16), exact in float32 for t, L < 2^24.
 __device__ __forceinline__ float taper_w(float tf, float Lf) {
@@ -80,15 +110,19 @@ struct Item {
   int g;           // segment
   int64_t tstart;  // global sample index of tile[0]
   const float *xrow;
+  int64_t L;       // this row's length
 };
 
-__device__ __forceinline__ Item make_item(int64_t item, int nseg, int64_t B, int64_t ld,
-                                          const float *ref, const float *deg) {
+__device__ __forceinline__ Item make_item(int64_t item, int nseg, int64_t B, int64_t ld, int64_t L,
+                                          const int32_t *__restrict__ lens, const float *ref,
+                                          const float *deg) {
   Item it;
   it.s = item / nseg;
   it.g = (int)(item - it.s * nseg);
   it.tstart = (int64_t)it.g * OWN - WARM;
-  it.xrow = (it.s < B) ? ref + it.s * ld : deg + (it.s - B) * ld;
+  const int64_t b = (it.s < B) ? it.s : it.s - B;
+  it.xrow = ((it.s < B) ? ref : deg) + b * ld;
+  it.L = row_length(lens, b, L);
   return it;
 }
 
@@ -97,7 +131,8 @@ __device__ __forceinline__ Item make_item(int64_t item, int nseg, int64_t B, int
 // the 32-bit offset; t >= ceil4(L)) return zeros from the hardware range check.  Samples in
 // [L, ceil4(L)) may hold anything: both filters are causal and every output at t >= L is
 // masked, so they cannot reach a result (rows must be readable up to ceil4(L), include/fsem.h).
-__device__ __forceinline__ void prefetch(const Item &it, int64_t L, int tid, float4 pre[PF]) {
+__device__ __forceinline__ void prefetch(const Item &it, int tid, float4 pre[PF]) {
+  const int64_t L = it.L;
   const uint64_t base = reinterpret_cast<uint64_t>(it.xrow);
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base);
   const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
@@ -181,9 +216,9 @@ __device__ __forceinline__ float iir_pass2(float4 *__restrict__ w4, float z[NS],
 // Persistent: each workgroup walks items (signal, segment) = blockIdx.x, +gridDim.x, ...;
 // the next item's tile is in flight in registers while the current one is processed.
 __global__ void __launch_bounds__(PT, 2)
-    pesq_front(const float *__restrict__ ref, const float *__restrict__ deg, int64_t B, int64_t L,
-               int64_t ld, int F, int nseg, int npseg, int64_t nitems, float *__restrict__ bark,
-               float *__restrict__ ppart) {
+    pesq_front(const float *__restrict__ ref, const float *__restrict__ deg, int64_t B, int64_t Lcap,
+               int64_t ld, const int32_t *__restrict__ lens, int F, int nseg, int64_t nitems,
+               float *__restrict__ bark, float *__restrict__ ppart) {
   __shared__ __attribute__((aligned(16))) float tile[TILE];
   __shared__ __attribute__((aligned(16))) float xbuf[XBUF];
   __shared__ float red[8];
@@ -210,10 +245,18 @@ __global__ void __launch_bounds__(PT, 2)
 
   float4 pre[PF];
   int64_t item = blockIdx.x;
-  if (item < nitems) prefetch(make_item(item, nseg, B, ld, ref, deg), L, tid, pre);
+  if (item < nitems) prefetch(make_item(item, nseg, B, ld, Lcap, lens, ref, deg), tid, pre);
 
   for (; item < nitems; item += gridDim.x) {
-    const Item it = make_item(item, nseg, B, ld, ref, deg);
+    const Item it = make_item(item, nseg, B, ld, Lcap, lens, ref, deg);
+    const int64_t L = it.L;
+    const Geometry rg = geometry(L);  // this row's geometry (== the launch's without lengths)
+    if (it.g >= rg.nseg) {  // segment past this row's end: no samples, no frames
+      if (tid == 0) ppart[it.s * nseg + it.g] = 0.f;
+      const int64_t nxt = item + gridDim.x;
+      if (nxt < nitems) prefetch(make_item(nxt, nseg, B, ld, Lcap, lens, ref, deg), tid, pre);
+      continue;
+    }
     STAMP(0);
     {
       float4 *t4 = reinterpret_cast<float4 *>(tile);
@@ -287,7 +330,7 @@ __global__ void __launch_bounds__(PT, 2)
 
     // ---------------------------------------------------------------- IIR pass 2
     {
-      const int64_t own_len = (g == nseg - 1) ? L - (int64_t)g * OWN : min((int64_t)OWN, L - (int64_t)g * OWN);
+      const int64_t own_len = (g == rg.nseg - 1) ? L - (int64_t)g * OWN : min((int64_t)OWN, L - (int64_t)g * OWN);
       const int own_lo = WARM - CH * tid, own_hi = WARM + (int)own_len - CH * tid;  // chunk-local
       const int lim = (int)min((int64_t)CH, max((int64_t)0, L - t_lane));       // y = 0 from here
       float4 *w4 = reinterpret_cast<float4 *>(tile + CH * tid);
@@ -307,11 +350,11 @@ __global__ void __launch_bounds__(PT, 2)
     // phases (the IIR phases above run without the prefetch registers live)
     {
       const int64_t nxt = item + gridDim.x;
-      if (nxt < nitems) prefetch(make_item(nxt, nseg, B, ld, ref, deg), L, tid, pre);
+      if (nxt < nitems) prefetch(make_item(nxt, nseg, B, ld, Lcap, lens, ref, deg), tid, pre);
     }
 
     // ---------------------------------------------------------------- FFT rounds
-    const int nfr = min(NF, F - g * NF);  // valid frames in this segment
+    const int nfr = min(NF, rg.F - g * NF);  // valid frames in this segment
     float2 *wbuf = reinterpret_cast<float2 *>(xbuf) + wave * kFftBuf;
     const int nrounds = nfr > 0 ? (nfr + 7) / 8 : 0;
     for (int rd = 0; rd < nrounds; ++rd) {
@@ -479,8 +522,8 @@ __device__ __forceinline__ void stage_chunk(float *__restrict__ dst, const float
 }
 
 __global__ void __launch_bounds__(BT)
-    pesq_back(const float *__restrict__ bark, const float *__restrict__ power, int64_t B, int64_t L,
-              int F, float *__restrict__ scratch, float *__restrict__ mos) {
+    pesq_back(const float *__restrict__ bark, const float *__restrict__ power, int64_t B, int64_t Lcap,
+              const int32_t *__restrict__ lens, int Fcap, float *__restrict__ scratch, float *__restrict__ mos) {
   __shared__ float C[BC * BLD], N[BC * BLD];
   __shared__ float ratio[NBARK];
   __shared__ float frs[BC + 1];
@@ -488,9 +531,15 @@ __global__ void __launch_bounds__(BT)
   __shared__ float bsum[2][2][64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t b = blockIdx.x;
-  const float *__restrict__ bc = bark + (b * (int64_t)F) * NBARK;
-  const float *__restrict__ bn = bark + ((b + B) * (int64_t)F) * NBARK;
-  float *__restrict__ silent = scratch + b * (int64_t)F * 4;
+  const int64_t L = row_length(lens, b, Lcap);
+  const int F = frames_of(L);  // this utterance's frames; rows are laid out with stride Fcap
+  if (F < 20) {  // the reference's unfold(1, 20, 10) raises here (PESQ.py:169)
+    if (tid == 0) mos[b] = __builtin_nanf("");
+    return;
+  }
+  const float *__restrict__ bc = bark + (b * (int64_t)Fcap) * NBARK;
+  const float *__restrict__ bn = bark + ((b + B) * (int64_t)Fcap) * NBARK;
+  float *__restrict__ silent = scratch + b * (int64_t)Fcap * 4;
   float *__restrict__ afpc = silent + F;
   float *__restrict__ sym = afpc + F;
   float *__restrict__ asym = sym + F;
@@ -624,28 +673,6 @@ __global__ void __launch_bounds__(BT)
   }
 }
 
-inline int frames_of(int64_t L) {
-  const int64_t Lp = L + (L % 256);  // PESQ.py:128-130: pad by L % 256 (sic)
-  if (Lp < 512) return 0;
-  return (int)(1 + (Lp - 512) / 256);
-}
-
-struct Geometry {
-  int F, nfseg, npseg, nseg;
-};
-
-// Segment g owns band-pass power samples [g*OWN, (g+1)*OWN); the LAST segment owns
-// [g*OWN, L), which its tile must cover: L - (nseg-1)*OWN <= TILE - WARM.
-inline Geometry geometry(int64_t L) {
-  Geometry g;
-  g.F = frames_of(L);
-  g.nfseg = (g.F + NF - 1) / NF;
-  const int64_t span = TILE - WARM;
-  g.npseg = L <= span ? 1 : (int)((L - span + OWN - 1) / OWN) + 1;
-  g.nseg = g.nfseg > g.npseg ? g.nfseg : g.npseg;
-  return g;
-}
-
 }  // namespace pesq
 }  // namespace fsem
 
@@ -677,11 +704,11 @@ extern "C" size_t fsem_pesq_workspace_bytes(int64_t batch, int64_t length) {
 }
 
 extern "C" int fsem_pesq_front_f32(const float *ref, const float *deg, int64_t batch, int64_t length,
-                                   int64_t ld, float *bark, float *power, void *ws, size_t ws_bytes,
-                                   void *stream) {
+                                   int64_t ld, const int32_t *lengths, float *bark, float *power, void *ws,
+                                   size_t ws_bytes, void *stream) {
   if (!ref || !deg || !bark || !power || batch <= 0 || length <= 0 || ld < length) return FSEM_EINVAL;
   const pesq::Geometry g = pesq::geometry(length);
-  if (g.F < 20) return FSEM_ESHORT;
+  if (g.F < 20 && !lengths) return FSEM_ESHORT;
   if (ws_bytes < fsem_pesq_front_workspace_bytes(batch, length) || !ws) return FSEM_EWORKSPACE;
   const int64_t nitems = 2 * batch * (int64_t)g.nseg;
   int dev = 0, ncu = 256;
@@ -690,7 +717,7 @@ extern "C" int fsem_pesq_front_f32(const float *ref, const float *deg, int64_t b
   float *ppart = static_cast<float *>(ws);
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(pesq::pesq_front, dim3((unsigned)grid), dim3(pesq::PT), 0, st, ref, deg, batch,
-                     length, ld, g.F, g.nseg, g.npseg, nitems, bark, ppart);
+                     length, ld, lengths, g.F, g.nseg, nitems, bark, ppart);
   FSEM_CHECK_LAUNCH();
   hipLaunchKernelGGL(pesq::pesq_power_sum, dim3((unsigned)((2 * batch + 255) / 256)), dim3(256), 0, st,
                      ppart, g.nseg, 2 * batch, power);
@@ -704,23 +731,25 @@ extern "C" size_t fsem_pesq_back_workspace_bytes(int64_t batch, int64_t length) 
 }
 
 extern "C" int fsem_pesq_back_f32(const float *bark, const float *power, int64_t batch, int64_t length,
-                                  float *mos, void *ws, size_t ws_bytes, void *stream) {
+                                  const int32_t *lengths, float *mos, void *ws, size_t ws_bytes,
+                                  void *stream) {
   if (!bark || !power || !mos || batch <= 0 || length <= 0) return FSEM_EINVAL;
   const pesq::Geometry g = pesq::geometry(length);
-  if (g.F < 20) return FSEM_ESHORT;
+  if (g.F < 20 && !lengths) return FSEM_ESHORT;
   if (!ws || ws_bytes < fsem_pesq_back_workspace_bytes(batch, length)) return FSEM_EWORKSPACE;
   if (batch > 0x7fffffff) return FSEM_EINVAL;
   hipLaunchKernelGGL(pesq::pesq_back, dim3((unsigned)batch), dim3(pesq::BT), 0, (hipStream_t)stream, bark,
-                     power, batch, length, g.F, static_cast<float *>(ws), mos);
+                     power, batch, length, lengths, g.F, static_cast<float *>(ws), mos);
   FSEM_CHECK_LAUNCH();
   return FSEM_OK;
 }
 
 extern "C" int fsem_pesq_wb_f32(const float *ref, const float *deg, int64_t batch, int64_t length,
-                                int64_t ld, float *mos, void *ws, size_t ws_bytes, void *stream) {
+                                int64_t ld, const int32_t *lengths, float *mos, void *ws, size_t ws_bytes,
+                                void *stream) {
   if (!ref || !deg || !mos || batch <= 0 || length <= 0 || ld < length) return FSEM_EINVAL;
   const pesq::Geometry g = pesq::geometry(length);
-  if (g.F < 20) return FSEM_ESHORT;
+  if (g.F < 20 && !lengths) return FSEM_ESHORT;
   if (!ws || ws_bytes < fsem_pesq_workspace_bytes(batch, length)) return FSEM_EWORKSPACE;
   char *p = static_cast<char *>(ws);
   const size_t front = fsem_pesq_front_workspace_bytes(batch, length);
@@ -728,8 +757,8 @@ extern "C" int fsem_pesq_wb_f32(const float *ref, const float *deg, int64_t batc
   p += front + align_up(sizeof(float) * (size_t)(2 * batch) * (size_t)g.F * pesq::NBARK, 256);
   float *power = reinterpret_cast<float *>(p);
   p += align_up(sizeof(float) * (size_t)(2 * batch), 256);
-  int rc = fsem_pesq_front_f32(ref, deg, batch, length, ld, bark, power, ws, front, stream);
+  int rc = fsem_pesq_front_f32(ref, deg, batch, length, ld, lengths, bark, power, ws, front, stream);
   if (rc != FSEM_OK) return rc;
-  return fsem_pesq_back_f32(bark, power, batch, length, mos, p,
+  return fsem_pesq_back_f32(bark, power, batch, length, lengths, mos, p,
                             fsem_pesq_back_workspace_bytes(batch, length), stream);
 }

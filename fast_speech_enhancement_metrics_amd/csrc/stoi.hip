@@ -30,6 +30,26 @@ constexpr int VF = 64;     // VAD frames per workgroup
 constexpr int TF = 32;     // STFT frames per workgroup
 constexpr float kClip = 1.0f + 5.62341325190349f;  // 1 + 10^(-beta/20), beta = -15 (STOI.py:136-137)
 
+// Per-row lengths: row b holds lens[b] input samples (clamped to [0, ncap]) when lens is
+// given, else ncap.  Its 10 kHz length is that of the reference's resampler on the unpadded
+// row, ceil(n * nw / orig) (torchaudio Resample, base.py:20), and its VAD frame count
+// 1 + (L10 - 256) / 128 (STOI.py:92-94).
+struct Rows {
+  const int32_t *lens;
+  int64_t ncap;
+  int orig, nw;  // reduced rate pair (1, 1 for 10 kHz input)
+  __device__ __forceinline__ int64_t n(int64_t b) const {
+    if (!lens) return ncap;
+    const int64_t v = lens[b];
+    return v < 0 ? 0 : (v > ncap ? ncap : v);
+  }
+  __device__ __forceinline__ int64_t l10(int64_t b) const { return (n(b) * nw + orig - 1) / orig; }
+  __device__ __forceinline__ int nv(int64_t b) const {
+    const int64_t L10 = l10(b);
+    return L10 >= 256 ? (int)((L10 - 256) / 128 + 1) : 0;
+  }
+};
+
 struct Src {
   const float *x;  // input row base (clean or denoised)
   int64_t n;       // input length at the input rate
@@ -54,13 +74,12 @@ constexpr int NG = YT / 5 + 2;                 // polyphase groups per item
 constexpr int XT4 = (8 * NG + 32) / 4;         // float4s of 16 kHz input staged per item
 constexpr int XPF = (XT4 + 255) / 256;         // prefetch float4s per thread
 __global__ void __launch_bounds__(256, 2)
-    stoi_resample_vad16(const float *__restrict__ ref, const float *__restrict__ deg, int64_t n_in, int64_t ld,
-                        int64_t L10, int NV, int nchunk, int64_t nitems, float *__restrict__ y10, int64_t y_ld,
+    stoi_resample_vad16(const float *__restrict__ ref, const float *__restrict__ deg, Rows rows, int64_t ld,
+                        int nchunk, int64_t nitems, float *__restrict__ y10, int64_t y_ld,
                         float *__restrict__ energy, int nv_ld) {
   __shared__ __attribute__((aligned(16))) float xin[XPF * 256 * 4 + 4];
   __shared__ __attribute__((aligned(16))) float ytile[YT + 8];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint32_t nbytes = (uint32_t)(((n_in + 3) & ~(int64_t)3) * 4);
   auto item_src = [&](int64_t item, int64_t &b, int &chunk, int &sig, int64_t &o0, int64_t &i0) {
     sig = (int)(item & 1);
     const int64_t bc = item >> 1;
@@ -73,6 +92,8 @@ __global__ void __launch_bounds__(256, 2)
     int64_t b, o0, i0;
     int chunk, sig;
     item_src(item, b, chunk, sig, o0, i0);
+    const int64_t n_in = rows.n(b);
+    const uint32_t nbytes = (uint32_t)(((n_in + 3) & ~(int64_t)3) * 4);
     const float *row = (sig == 0 ? ref : deg) + b * ld;
     const uint64_t base = reinterpret_cast<uint64_t>(row);
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base);
@@ -102,6 +123,12 @@ __global__ void __launch_bounds__(256, 2)
     int64_t b, o0, i0;
     int chunk, sig;
     item_src(item, b, chunk, sig, o0, i0);
+    const int64_t L10 = rows.l10(b);
+    if (o0 >= L10) {  // chunk past this row's end
+      if (item + gridDim.x < nitems) prefetch(item + gridDim.x, pre);
+      continue;
+    }
+    const int NV = rows.nv(b);
     // staged at +2 floats: group m's 28 taps then start 16-byte aligned at xin[8(m - m0) + 4]
     float2 *x2 = reinterpret_cast<float2 *>(xin + 2);
 #pragma unroll
@@ -169,13 +196,16 @@ __global__ void __launch_bounds__(256, 2)
 constexpr int VF3 = 32;
 constexpr int YT3 = VF3 * 128 + 128;
 __global__ void __launch_bounds__(256)
-    stoi_resample_vad(const float *__restrict__ ref, const float *__restrict__ deg, int64_t n_in, int64_t ld,
-                      int64_t L10, int NV, int mode, ResampleKernel rk, float *__restrict__ y10, int64_t y_ld,
+    stoi_resample_vad(const float *__restrict__ ref, const float *__restrict__ deg, Rows rows, int64_t ld,
+                      int mode, ResampleKernel rk, float *__restrict__ y10, int64_t y_ld,
                       float *__restrict__ energy, int nv_ld) {
   __shared__ __attribute__((aligned(16))) float ytile[YT3];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t b = blockIdx.y;
   const int64_t o0 = (int64_t)blockIdx.x * (VF3 * 128);
+  const int64_t n_in = rows.n(b), L10 = rows.l10(b);
+  const int NV = rows.nv(b);
+  if (o0 >= L10) return;
   const int64_t o_end = min(o0 + (int64_t)YT3, L10);
   const int ny = (int)(o_end - o0);
   const int nw_own = (int)min((int64_t)(VF3 * 128), L10 - o0);
@@ -205,12 +235,13 @@ __global__ void __launch_bounds__(256)
 }
 
 __global__ void __launch_bounds__(256)
-    stoi_select(const float *__restrict__ energy, int nv_ld, int NV, int *__restrict__ idx,
+    stoi_select(const float *__restrict__ energy, int nv_ld, Rows rows, int *__restrict__ idx,
                 int *__restrict__ kept) {
   __shared__ float red[8];
   __shared__ int wcount[4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t b = blockIdx.x;
+  const int NV = rows.nv(b);
   const float *e = energy + b * nv_ld;
   float m = -INFINITY;
   for (int i = tid; i < NV; i += 256) m = fmaxf(m, e[i]);
@@ -234,7 +265,7 @@ __global__ void __launch_bounds__(256)
 }
 
 __global__ void __launch_bounds__(256)
-    stoi_tob(const float *__restrict__ y10, int64_t y_ld, int64_t B, int64_t L10, const int *__restrict__ idx,
+    stoi_tob(const float *__restrict__ y10, int64_t y_ld, int64_t B, Rows rows, const int *__restrict__ idx,
              const int *__restrict__ kept, int nv_ld, float *__restrict__ tob, int64_t tmax) {
   __shared__ __attribute__((aligned(16))) float blk[2][TF + 1][128];
   __shared__ __attribute__((aligned(16))) float xbuf[4 * 2 * kFftBuf];
@@ -242,6 +273,7 @@ __global__ void __launch_bounds__(256)
   const int64_t b = blockIdx.y;
   const int n = kept[b];
   const int T = n - 2;  // STFT frames of the overlap-added signal: 1 + ((n+1)*128 - 512)/128
+  const int64_t L10 = rows.l10(b);
   const int k0 = blockIdx.x * TF;
   if (k0 >= T) return;
   const int kend = min(k0 + TF, T);
@@ -505,14 +537,15 @@ inline size_t ws_bytes(int64_t B, const Geometry &g) {
   return s;
 }
 
-inline int run(const float *ref, const float *deg, int64_t B, int64_t length, int64_t ld, int32_t sr,
-               float *stoi_out, float *estoi_out, int32_t *kept_out, float *tob_out, int64_t tob_ld,
-               void *ws, size_t ws_size, hipStream_t st) {
+inline int run(const float *ref, const float *deg, int64_t B, int64_t length, int64_t ld,
+               const int32_t *lengths, int32_t sr, float *stoi_out, float *estoi_out, int32_t *kept_out,
+               float *tob_out, int64_t tob_ld, void *ws, size_t ws_size, hipStream_t st) {
   Geometry g;
   ResampleKernel rk;
   int rc = make_geometry(length, sr, &g, &rk);
   if (rc != FSEM_OK) return rc;
-  if (g.NV <= 0) return FSEM_ESHORT;
+  if (g.NV <= 0 && !lengths) return FSEM_ESHORT;  // with lengths: NaN rows instead
+  const Rows rows{lengths, length, rk.orig, rk.nw};
   if (!ws || ws_size < ws_bytes(B, g)) return FSEM_EWORKSPACE;
   if (B > 65535) return FSEM_EINVAL;
   char *p = static_cast<char *>(ws);
@@ -537,18 +570,17 @@ inline int run(const float *ref, const float *deg, int64_t B, int64_t length, in
     int dev = 0, ncu = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     const int64_t grid = nitems < (int64_t)ncu * 3 ? nitems : (int64_t)ncu * 3;  // 3 resident per CU
-    hipLaunchKernelGGL(stoi_resample_vad16, dim3((unsigned)grid), dim3(256), 0, st, ref, deg, length, ld, g.L10,
-                       g.NV, nchunk, nitems, y10, g.y_ld, energy, g.nv_ld);
+    hipLaunchKernelGGL(stoi_resample_vad16, dim3((unsigned)grid), dim3(256), 0, st, ref, deg, rows, ld, nchunk,
+                       nitems, y10, g.y_ld, energy, g.nv_ld);
   } else {
     hipLaunchKernelGGL(stoi_resample_vad, dim3((unsigned)((g.L10 + VF3 * 128 - 1) / (VF3 * 128)), (unsigned)B),
-                       dim3(256), 0, st, ref, deg, length, ld, g.L10, g.NV, g.mode, rk, y10, g.y_ld, energy,
-                       g.nv_ld);
+                       dim3(256), 0, st, ref, deg, rows, ld, g.mode, rk, y10, g.y_ld, energy, g.nv_ld);
   }
   FSEM_CHECK_LAUNCH();
-  hipLaunchKernelGGL(stoi_select, dim3((unsigned)B), dim3(256), 0, st, energy, g.nv_ld, g.NV, idx, kept);
+  hipLaunchKernelGGL(stoi_select, dim3((unsigned)B), dim3(256), 0, st, energy, g.nv_ld, rows, idx, kept);
   FSEM_CHECK_LAUNCH();
   hipLaunchKernelGGL(stoi_tob, dim3((unsigned)((g.tmax + TF - 1) / TF), (unsigned)B), dim3(256), 0, st, y10,
-                     g.y_ld, B, g.L10, idx, kept, g.nv_ld, tob, tmax);
+                     g.y_ld, B, rows, idx, kept, g.nv_ld, tob, tmax);
   FSEM_CHECK_LAUNCH();
   if (stoi_out) {
     hipLaunchKernelGGL(stoi_seg, dim3((unsigned)B), dim3(SEG_T), 0, st, tob, B, tmax, kept, stoi_out,
@@ -571,11 +603,11 @@ extern "C" size_t fsem_stoi_workspace_bytes(int64_t batch, int64_t length, int32
 }
 
 extern "C" int fsem_stoi_f32(const float *ref, const float *deg, int64_t batch, int64_t length, int64_t ld,
-                             int32_t sample_rate, float *stoi_out, float *estoi_out, void *ws, size_t ws_bytes,
-                             void *stream) {
+                             const int32_t *lengths, int32_t sample_rate, float *stoi_out, float *estoi_out,
+                             void *ws, size_t ws_bytes, void *stream) {
   if (!ref || !deg || !stoi_out || !estoi_out || batch <= 0 || length <= 0 || ld < length) return FSEM_EINVAL;
-  return stoi::run(ref, deg, batch, length, ld, sample_rate, stoi_out, estoi_out, nullptr, nullptr, 0, ws,
-                   ws_bytes, (hipStream_t)stream);
+  return stoi::run(ref, deg, batch, length, ld, lengths, sample_rate, stoi_out, estoi_out, nullptr, nullptr, 0,
+                   ws, ws_bytes, (hipStream_t)stream);
 }
 
 extern "C" int fsem_stoi_tob_f32(const float *ref10, const float *deg10, int64_t batch, int64_t length10,
@@ -587,8 +619,8 @@ extern "C" int fsem_stoi_tob_f32(const float *ref10, const float *deg10, int64_t
   int rc = stoi::make_geometry(length10, 10000, &g, &rk);
   if (rc != FSEM_OK) return rc;
   if (tmax < g.tmax) return FSEM_EINVAL;
-  return stoi::run(ref10, deg10, batch, length10, ld, 10000, nullptr, nullptr, kept, tob, tmax, ws, ws_bytes,
-                   (hipStream_t)stream);
+  return stoi::run(ref10, deg10, batch, length10, ld, nullptr, 10000, nullptr, nullptr, kept, tob, tmax, ws,
+                   ws_bytes, (hipStream_t)stream);
 }
 
 extern "C" const char *fsem_strerror(int code) {
@@ -603,4 +635,4 @@ extern "C" const char *fsem_strerror(int code) {
   }
 }
 
-extern "C" int fsem_version(void) { return 1; }
+extern "C" int fsem_version(void) { return 2; }

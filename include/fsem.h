@@ -17,6 +17,12 @@
  *  - signals are float32 rows: element (b, t) of a batch lives at ptr[b * ld + t]; the
  *    PESQ and STOI entries read rows in 16-byte pieces, so each row must be readable up to
  *    ceil4(length) floats (values past `length` are never used);
+ *  - per-row lengths (variable-length batches): the PESQ and STOI entries take
+ *    `lengths`, a DEVICE int32[batch] array or NULL.  NULL means every row has `length`
+ *    samples.  Otherwise row b holds lengths[b] samples (clamped to [0, length]; `length`
+ *    is then the row capacity, sizing workspace and layouts) and its result is that of the
+ *    reference called on the unpadded row alone; rows too short for the metric give NaN
+ *    (instead of FSEM_ESHORT, which only the whole-batch form returns);
  *  - return 0 on success or a negative FSEM_E* code (fsem_strerror() for text);
  *  - re-entrant across streams / devices (launches use the current HIP device).
  */
@@ -55,42 +61,49 @@ int fsem_resample_f32(const float *in, int64_t rows, int64_t n_in, int64_t ld_in
  * (get_disturbances :174-230 + MOS mapping :240-243) for 16 kHz input.
  *   ref, deg : [batch, length] float32 (row stride ld)  -- clean / denoised
  *   mos      : [batch] float32 output
+ *   lengths  : NULL or [batch] int32 per-row lengths (see Conventions)
  * FSEM_ESHORT when the padded length yields < 20 frames (the reference's
- * unfold(1, 20, 10) raises RuntimeError there, PESQ.py:169).
+ * unfold(1, 20, 10) raises RuntimeError there, PESQ.py:169); with `lengths`, such rows
+ * give NaN.
  */
 size_t fsem_pesq_workspace_bytes(int64_t batch, int64_t length);
 int fsem_pesq_frames(int64_t length);  /* F = 1 + (L + L%256 - 512) / 256 (PESQ.py:128-133) */
 int fsem_pesq_wb_f32(const float *ref, const float *deg, int64_t batch, int64_t length,
-                     int64_t ld, float *mos, void *ws, size_t ws_bytes, void *stream);
+                     int64_t ld, const int32_t *lengths, float *mos, void *ws, size_t ws_bytes,
+                     void *stream);
 
 /* Stage entries (same math, split for parity tests of intermediates):
  * front: replaces PESQ.align_level's filtered power (PESQ.py:92-98) and
  *        PESQ.get_bark_bands (PESQ.py:123-140) up to BarkFilterBank.forward
  *        (bark.py:203-204), BEFORE the level scale:
- *          bark  [2*batch, F, 49] float32 (rows 0..B-1 ref, B..2B-1 deg), unscaled
+ *          bark  [2*batch, F, 49] float32 (rows 0..B-1 ref, B..2B-1 deg), unscaled,
+ *                F = fsem_pesq_frames(length); a shorter row fills its first
+ *                fsem_pesq_frames(lengths[b]) frames
  *          power [2*batch] float32 = sum_t filtered^2 (not yet / (L+5120) / 1.04684)
  * back:  replaces PESQ.py:142-245 on those tensors -> mos [batch].
  */
 size_t fsem_pesq_front_workspace_bytes(int64_t batch, int64_t length);
 int fsem_pesq_front_f32(const float *ref, const float *deg, int64_t batch, int64_t length,
-                        int64_t ld, float *bark, float *power, void *ws, size_t ws_bytes,
-                        void *stream);
+                        int64_t ld, const int32_t *lengths, float *bark, float *power, void *ws,
+                        size_t ws_bytes, void *stream);
 size_t fsem_pesq_back_workspace_bytes(int64_t batch, int64_t length);
 int fsem_pesq_back_f32(const float *bark, const float *power, int64_t batch, int64_t length,
-                       float *mos, void *ws, size_t ws_bytes, void *stream);
+                       const int32_t *lengths, float *mos, void *ws, size_t ws_bytes,
+                       void *stream);
 
 /* ---------------------------------------------------------------- STOI / ESTOI
  * Whole-metric entry: replaces STOI.compute_stoi + compute_metric
  *   fast_se_metrics/STOI.py:153-205 (after BaseMetric resampling to 10 kHz,
  *   base.py:19-20, when sample_rate != 10000).
  *   ref, deg    : [batch, length] float32 at `sample_rate` (row stride ld)
+ *   lengths     : NULL or [batch] int32 per-row lengths at `sample_rate` (Conventions)
  *   stoi, estoi : [batch] float32 outputs; NaN where no 30-frame segment exists
  *                 (the reference warns there, STOI.py:163-165).
  */
 size_t fsem_stoi_workspace_bytes(int64_t batch, int64_t length, int32_t sample_rate);
 int fsem_stoi_f32(const float *ref, const float *deg, int64_t batch, int64_t length,
-                  int64_t ld, int32_t sample_rate, float *stoi, float *estoi, void *ws,
-                  size_t ws_bytes, void *stream);
+                  int64_t ld, const int32_t *lengths, int32_t sample_rate, float *stoi,
+                  float *estoi, void *ws, size_t ws_bytes, void *stream);
 
 /* Intermediates of the 10 kHz STOI pipeline for parity tests:
  *   kept  [batch] int32   -- frames kept by remove_silent_frames (STOI.py:88-111)

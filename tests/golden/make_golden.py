@@ -79,7 +79,67 @@ def stoi_case(name: str, batch: int, length: int, sr: int, seed: int, snr=(-5.0,
     print(name, out["stoi"], out["estoi"], out["kept"])
 
 
+def rate_case(name: str, batch: int, length: int, sr: int, seed: int):
+    """Uniform batch at a non-native rate: PESQ resamples sr -> 16 kHz, STOI sr -> 10 kHz in
+    BaseMetric.prepare_audio (base.py:19-20)."""
+    clean, noisy, snr_v = speech_like_pairs(batch, length, sr, seed=seed)
+    p = RefPESQ(sample_rate=sr, use_gpu=False)
+    pesq_s = np.array([d["PESQ"] for d in p(clean, noisy)], dtype=np.float64)
+    st = RefSTOI(sample_rate=sr, use_gpu=False)
+    torch.manual_seed(0)
+    res = st(clean, noisy)
+    out = dict(clean=to_int16(clean).numpy(), noisy=to_int16(noisy).numpy(), snr=snr_v.numpy(), sample_rate=sr,
+               pesq=pesq_s, stoi=np.array([d["STOI"] for d in res]), estoi=np.array([d["ESTOI"] for d in res]))
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
+    print(name, pesq_s, out["stoi"], out["estoi"])
+
+
+def varlen_case(name: str, lengths, sr: int, seed: int):
+    """Ragged batch: each utterance's expected score is the reference called on
+    that unpadded utterance ALONE; NaN where the reference rejects it (too short).  The stored
+    rows keep the signal past each length (not zeros) so the engine must ignore it."""
+    import warnings
+    cap = max(lengths)
+    clean, noisy, snr_v = speech_like_pairs(len(lengths), cap, sr, seed=seed)
+    p = RefPESQ(sample_rate=sr, use_gpu=False)
+    st = RefSTOI(sample_rate=sr, use_gpu=False)
+    pesq_s, stoi_s, estoi_s = [], [], []
+    for i, n in enumerate(lengths):
+        c, d = clean[i:i + 1, :n], noisy[i:i + 1, :n]
+        try:
+            pesq_s.append(p(c, d)[0]["PESQ"])
+        except RuntimeError:
+            pesq_s.append(float("nan"))
+        torch.manual_seed(0)
+        try:
+            with warnings.catch_warnings():
+                warnings.simplefilter("ignore")
+                r = st(c, d)[0]
+            stoi_s.append(r["STOI"])
+            estoi_s.append(r["ESTOI"])
+        except TypeError:
+            stoi_s.append(float("nan"))
+            estoi_s.append(float("nan"))
+    out = dict(clean=to_int16(clean).numpy(), noisy=to_int16(noisy).numpy(), snr=snr_v.numpy(), sample_rate=sr,
+               lengths=np.array(lengths, dtype=np.int32), pesq=np.array(pesq_s), stoi=np.array(stoi_s),
+               estoi=np.array(estoi_s))
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
+    print(name, out["pesq"], out["stoi"], out["estoi"])
+
+
+CASES = {
+    "rate_8k": lambda: rate_case("rate_8k", batch=3, length=24000, sr=8000, seed=11),
+    "varlen_16k": lambda: varlen_case("varlen_16k", [48000, 33333, 20001, 40960, 5000, 27003], sr=16000, seed=12),
+    "varlen_8k": lambda: varlen_case("varlen_8k", [24000, 16667, 11111], sr=8000, seed=13),
+}
+
 if __name__ == "__main__":
+    only = sys.argv[1:]
+    if only:
+        torch.set_num_threads(8)
+        for name in only:
+            CASES[name]()
+        sys.exit(0)
     torch.set_num_threads(8)
     pesq_case("pesq_3s", batch=4, length=48000, seed=1)
     pesq_case("pesq_ragged", batch=3, length=40077, seed=2)      # L % 256 != 0 (PESQ.py:128 quirk)
@@ -91,3 +151,5 @@ if __name__ == "__main__":
     stoi_case("stoi_16k", batch=4, length=48000, sr=16000, seed=6)   # resampler exercised
     stoi_case("stoi_16k_10s", batch=2, length=160000, sr=16000, seed=7)
     stoi_case("stoi_wide", batch=6, length=32000, sr=16000, seed=9, snr=(-10.0, 30.0))
+    for make in CASES.values():
+        make()

@@ -54,13 +54,13 @@ def test_pesq_frames_matches_reference_rule(lib, L):
 
 def test_invalid_arguments_are_rejected_without_launch(lib):
     null = None
-    assert lib.fsem_pesq_wb_f32(null, null, 4, 160000, 160000, null, null, 0, null) == -1
+    assert lib.fsem_pesq_wb_f32(null, null, 4, 160000, 160000, null, null, null, 0, null) == -1
     # too short (< 20 frames): the reference's unfold raises; we return FSEM_ESHORT
     p = ctypes.c_void_p(16)
-    assert lib.fsem_pesq_wb_f32(p, p, 1, 4000, 4000, p, p, 1 << 30, null) == -4
+    assert lib.fsem_pesq_wb_f32(p, p, 1, 4000, 4000, null, p, p, 1 << 30, null) == -4
     # workspace too small
-    assert lib.fsem_pesq_wb_f32(p, p, 4, 160000, 160000, p, p, 16, null) == -2
-    assert lib.fsem_stoi_f32(p, p, 4, 160000, 160000, 16000, p, p, p, 16, null) == -2
+    assert lib.fsem_pesq_wb_f32(p, p, 4, 160000, 160000, null, p, p, 16, null) == -2
+    assert lib.fsem_stoi_f32(p, p, 4, 160000, 160000, null, 16000, p, p, p, 16, null) == -2
     assert lib.fsem_stoi_workspace_bytes(4, 160000, 16000) > 0
     assert lib.fsem_pesq_workspace_bytes(4096, 160000) > 4096 * 2 * 624 * 49 * 4
 

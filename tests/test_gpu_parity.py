@@ -50,7 +50,7 @@ def test_pesq_front_bark_matches_reference(dev, name):
     bark = torch.empty(2 * B, F, 49, device=dev)
     power = torch.empty(2 * B, device=dev)
     ws = _native.workspace(lib.fsem_pesq_front_workspace_bytes(B, L), dev)
-    _native.check(lib.fsem_pesq_front_f32(c.data_ptr(), n.data_ptr(), B, L, ld, bark.data_ptr(), power.data_ptr(),
+    _native.check(lib.fsem_pesq_front_f32(c.data_ptr(), n.data_ptr(), B, L, ld, None, bark.data_ptr(), power.data_ptr(),
                                           ws.data_ptr(), ws.numel(), _native.stream_handle(dev)), "front")
     torch.cuda.synchronize()
     p = power.double().cpu().numpy() / (L + 5120) / 1.04684

@@ -1,0 +1,179 @@
+"""Variable-length batches and non-native input rates.
+
+Golden vectors (tests/golden/make_golden.py, the reference run in the build container):
+  rate_8k     uniform 8 kHz batch: PESQ(sample_rate=8000) resamples 8 -> 16 kHz, STOI 8 -> 10 kHz
+              (base.py:13,19-20);
+  varlen_16k  ragged 16 kHz batch, each expected score = the reference on that unpadded
+  varlen_8k   utterance alone (NaN where the reference rejects it as too short); rows keep the
+              signal past their length, which the engine must ignore.
+The CPU tests pin the oracle and the CPU mode; the gpu tests run the HIP engine through the
+drop-in API (list-of-utterances form and padded-tensor + lengths form).
+"""
+import warnings
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import pesq_oracle, stoi_oracle, ta
+from tests.conftest import load_golden
+
+VARLEN = ["varlen_16k", "varlen_8k"]
+PESQ_TOL, STOI_TOL = 5e-3, 5e-4  # engine vs reference (test_gpu_parity.py)
+
+
+def _oracle_row(g, b):
+    n = int(g["lengths"][b])
+    sr = int(g["sample_rate"])
+    c, d = g["clean_f"][b:b + 1, :n], g["noisy_f"][b:b + 1, :n]
+    c16 = ta.resample(c, sr, 16000) if sr != 16000 else c
+    d16 = ta.resample(d, sr, 16000) if sr != 16000 else d
+    try:
+        p = float(pesq_oracle.pesq(c16, d16)[0])
+    except (RuntimeError, ValueError, IndexError):
+        p = float("nan")
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        s, e = stoi_oracle.stoi(c, d, sr)
+    return p, float(s[0]), float(e[0])
+
+
+def _close_with_nans(got, want, atol):
+    got, want = np.asarray(got, dtype=np.float64), np.asarray(want, dtype=np.float64)
+    assert np.array_equal(np.isnan(got), np.isnan(want)), (got, want)
+    m = ~np.isnan(want)
+    np.testing.assert_allclose(got[m], want[m], atol=atol, rtol=0)
+
+
+# ------------------------------------------------------------------------------- oracle pin
+@pytest.mark.parametrize("name", VARLEN)
+def test_oracle_varlen_matches_reference(name):
+    g = load_golden(name)
+    rows = [_oracle_row(g, b) for b in range(len(g["lengths"]))]
+    _close_with_nans([r[0] for r in rows], g["pesq"], 2e-3)
+    _close_with_nans([r[1] for r in rows], g["stoi"], 1e-5)
+    _close_with_nans([r[2] for r in rows], g["estoi"], 1e-5)
+
+
+def test_oracle_8k_matches_reference():
+    g = load_golden("rate_8k")
+    c16, d16 = ta.resample(g["clean_f"], 8000, 16000), ta.resample(g["noisy_f"], 8000, 16000)
+    np.testing.assert_allclose(pesq_oracle.pesq(c16, d16), g["pesq"], atol=2e-3, rtol=0)
+    s, e = stoi_oracle.stoi(g["clean_f"], g["noisy_f"], 8000)
+    np.testing.assert_allclose(s, g["stoi"], atol=1e-5, rtol=0)
+    np.testing.assert_allclose(e, g["estoi"], atol=1e-5, rtol=0)
+
+
+def test_varlen_golden_has_short_rows():
+    g = load_golden("varlen_16k")
+    assert np.isnan(g["pesq"]).any() and np.isnan(g["stoi"]).any()  # the NaN contract is exercised
+    assert (g["lengths"] < g["clean"].shape[1]).sum() >= 4
+
+
+# ------------------------------------------------------------------------------- host logic
+def test_pad_batch_and_lengths():
+    from fast_speech_enhancement_metrics_amd.batching import as_lengths, pad_batch, resampled_lengths
+    c = [torch.ones(5), torch.ones(9)]
+    d = [torch.zeros(5), torch.zeros(9)]
+    pc, pd, lens = pad_batch(c, d)
+    assert pc.shape == (2, 12) and lens.tolist() == [5, 9] and lens.dtype == torch.int32
+    assert pc[0, 5:].abs().sum() == 0 and pc[1, :9].sum() == 9
+    with pytest.raises(Exception, match="same shape"):
+        pad_batch([torch.ones(5)], [torch.ones(6)])
+    with pytest.raises(ValueError):
+        as_lengths([3, 13], 2, 12)
+    assert resampled_lengths(torch.tensor([24000, 16667, 11111]), 8000, 16000).tolist() == [48000, 33334, 22222]
+    assert resampled_lengths(torch.tensor([16001]), 16000, 10000).tolist() == [10001]
+
+
+# ------------------------------------------------------------------------------- CPU mode
+def test_cpu_mode_8k_matches_reference():
+    from fast_speech_enhancement_metrics_amd import PESQ, STOI
+    g = load_golden("rate_8k")
+    c, d = torch.from_numpy(g["clean_f"]), torch.from_numpy(g["noisy_f"])
+    np.testing.assert_allclose([r["PESQ"] for r in PESQ(8000)(c, d)], g["pesq"], atol=2e-3, rtol=0)
+    res = STOI(8000)(c, d)
+    np.testing.assert_allclose([r["STOI"] for r in res], g["stoi"], atol=1e-4, rtol=0)
+    np.testing.assert_allclose([r["ESTOI"] for r in res], g["estoi"], atol=1e-4, rtol=0)
+
+
+@pytest.mark.parametrize("name", VARLEN)
+def test_cpu_mode_varlen_matches_reference(name):
+    from fast_speech_enhancement_metrics_amd import PESQ, STOI
+    g = load_golden(name)
+    sr = int(g["sample_rate"])
+    c, d, lens = torch.from_numpy(g["clean_f"]), torch.from_numpy(g["noisy_f"]), g["lengths"]
+    _close_with_nans([r["PESQ"] for r in PESQ(sr)(c, d, lengths=lens)], g["pesq"], 2e-3)
+    cl = [c[b, :n] for b, n in enumerate(lens)]
+    dl = [d[b, :n] for b, n in enumerate(lens)]
+    res = STOI(sr)(cl, dl)
+    _close_with_nans([r["STOI"] for r in res], g["stoi"], 1e-4)
+    _close_with_nans([r["ESTOI"] for r in res], g["estoi"], 1e-4)
+
+
+# ------------------------------------------------------------------------------- GPU engine
+@pytest.mark.gpu
+def test_gpu_8k_matches_reference():
+    from fast_speech_enhancement_metrics_amd import PESQ, STOI
+    g = load_golden("rate_8k")
+    c, d = torch.from_numpy(g["clean_f"]), torch.from_numpy(g["noisy_f"])
+    np.testing.assert_allclose([r["PESQ"] for r in PESQ(8000, use_gpu=True)(c, d)], g["pesq"], atol=PESQ_TOL, rtol=0)
+    res = STOI(8000, use_gpu=True)(c, d)
+    np.testing.assert_allclose([r["STOI"] for r in res], g["stoi"], atol=STOI_TOL, rtol=0)
+    np.testing.assert_allclose([r["ESTOI"] for r in res], g["estoi"], atol=STOI_TOL, rtol=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", VARLEN)
+@pytest.mark.parametrize("form", ["lists", "lengths"])
+def test_gpu_varlen_matches_reference(name, form):
+    from fast_speech_enhancement_metrics_amd import PESQ, STOI
+    g = load_golden(name)
+    sr = int(g["sample_rate"])
+    c, d, lens = torch.from_numpy(g["clean_f"]), torch.from_numpy(g["noisy_f"]), g["lengths"]
+    if form == "lists":
+        args = ([c[b, :n] for b, n in enumerate(lens)], [d[b, :n] for b, n in enumerate(lens)])
+        kw = {}
+    else:  # padded rows holding signal past each length: must be ignored
+        args, kw = (c, d), {"lengths": torch.from_numpy(lens)}
+    _close_with_nans([r["PESQ"] for r in PESQ(sr, use_gpu=True)(*args, **kw)], g["pesq"], PESQ_TOL)
+    res = STOI(sr, use_gpu=True)(*args, **kw)
+    _close_with_nans([r["STOI"] for r in res], g["stoi"], STOI_TOL)
+    _close_with_nans([r["ESTOI"] for r in res], g["estoi"], STOI_TOL)
+
+
+@pytest.mark.gpu
+def test_gpu_full_lengths_equal_uniform():
+    """lengths == capacity for every row gives bit-identical scores to the uniform call."""
+    from fast_speech_enhancement_metrics_amd import PESQ, STOI
+    g = load_golden("pesq_ragged")
+    c = torch.from_numpy(g["clean_f"]).cuda()
+    d = torch.from_numpy(g["noisy_f"]).cuda()
+    lens = torch.full((c.shape[0],), c.shape[1], dtype=torch.int32)
+    p = PESQ(16000, use_gpu=True)
+    assert torch.equal(p.scores(c, d), p.scores(c, d, lengths=lens))
+    s = STOI(16000, use_gpu=True)
+    a, b = s.scores(c, d, 16000), s.scores(c, d, 16000, lengths=lens)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+
+
+@pytest.mark.gpu
+def test_gpu_varlen_large_mixed_batch():
+    """A ragged batch of 64 utterances (1-12 s at 16 kHz) against per-utterance uniform calls
+    of the engine itself (shared kernels, per-row geometry)."""
+    from fast_speech_enhancement_metrics_amd import PESQ, STOI
+    from fast_speech_enhancement_metrics_amd.synthetic import speech_like_pairs
+    rng = np.random.default_rng(3)
+    lens = rng.integers(16000, 192000, size=64)
+    lens[:4] = [192000, 16000, 16001, 40077]
+    cap = int(lens.max())
+    c, d, _ = speech_like_pairs(64, cap, 16000, seed=21, device="cuda")
+    p, s = PESQ(16000, use_gpu=True), STOI(16000, use_gpu=True)
+    mos = p.scores(c, d, lengths=torch.from_numpy(lens.astype(np.int32))).cpu().numpy()
+    st, es = (t.cpu().numpy() for t in s.scores(c, d, 16000, lengths=torch.from_numpy(lens.astype(np.int32))))
+    for b in range(0, 64, 7):
+        n = int(lens[b])
+        m1 = p.scores(c[b:b + 1, :n].contiguous(), d[b:b + 1, :n].contiguous()).item()
+        s1, e1 = (t.item() for t in s.scores(c[b:b + 1, :n].contiguous(), d[b:b + 1, :n].contiguous(), 16000))
+        assert abs(mos[b] - m1) < 1e-4, (b, mos[b], m1)
+        assert abs(st[b] - s1) < 1e-5 and abs(es[b] - e1) < 1e-5, (b, st[b], s1)

@@ -27,7 +27,7 @@ h = torch.cuda.current_stream().cuda_stream
 
 
 def front():
-    _native.check(lib.fsem_pesq_front_f32(c.data_ptr(), n.data_ptr(), B, L, L, bark.data_ptr(), power.data_ptr(),
+    _native.check(lib.fsem_pesq_front_f32(c.data_ptr(), n.data_ptr(), B, L, L, None, bark.data_ptr(), power.data_ptr(),
                                           ws.data_ptr(), ws.numel(), h), "front")
 
 
