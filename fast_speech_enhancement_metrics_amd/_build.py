@@ -18,7 +18,7 @@ LIBDIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIBDIR, "libfsem.so")
 STAMP_LIB = os.path.join(LIBDIR, "libfsem_stamps.so")  # diagnostic build (tools/stamps.py)
 SOURCES = ["pesq.hip", "stoi.hip", "resample.hip"]
-HEADERS = ["fsem_common.h", "fsem_fft.h", "fsem_resample.h", "fsem_tables.inc"]
+HEADERS = ["fsem_common.h", "fsem_fft.h", "fsem_internal.h", "fsem_resample.h", "fsem_tables.inc"]
 ARCH = os.environ.get("FSEM_OFFLOAD_ARCH", "gfx950")
 
 

@@ -1,0 +1,17 @@
+// Internal (non-exported, C++) entry points shared between the engine's translation units;
+// the joint PESQ + STOI entry (fsem_pesq_stoi_f32, stoi.hip) composes them.
+#pragma once
+#include "fsem_common.h"
+
+namespace fsem {
+namespace pesq {
+// pesq_front + power sums; with y10 != nullptr also writes the rows' 10 kHz resampled signals
+// ([2*batch, y_ld], row 2b = clean b, 2b+1 = denoised b) from the same LDS tiles.
+int launch_front(const float *ref, const float *deg, int64_t batch, int64_t length, int64_t ld,
+                 const int32_t *lengths, float *bark, float *power, void *ws, size_t ws_bytes, float *y10,
+                 int64_t y_ld, hipStream_t st);
+// whole PESQ-wb (front + back), optionally emitting y10 as above
+int run_wb(const float *ref, const float *deg, int64_t batch, int64_t length, int64_t ld, const int32_t *lengths,
+           float *mos, void *ws, size_t ws_bytes, float *y10, int64_t y_ld, hipStream_t st);
+}  // namespace pesq
+}  // namespace fsem

@@ -32,6 +32,7 @@
 #include <algorithm>
 
 #include "fsem_fft.h"
+#include "fsem_internal.h"
 
 namespace fsem {
 
@@ -213,17 +214,77 @@ __device__ __forceinline__ float iir_pass2(float4 *__restrict__ w4, float z[NS],
   return acc;
 }
 
+// Joint mode (fsem_pesq_stoi_f32): STOI's 16 -> 10 kHz resampler (BaseMetric.prepare_audio,
+// base.py:19-20) runs on the same LDS tile, so the input is read from HBM once for both
+// metrics.  Segment g owns 10 kHz outputs [g*OWN10, (g+1)*OWN10) (the last: up to the row's
+// 10 kHz length), i.e. polyphase groups m = g*OWN/8 + j whose 28 taps x[8m - 10 + t] sit at
+// tile[WARM - 10 + 8j + t]; same tap order as stoi_resample_vad16, so bitwise the same y10.
+constexpr int OWN10 = OWN / 8 * 5;  // 7680
+constexpr int TILE_PAD = 16;        // zeros after the tile: the last segment's final taps
+static_assert(OWN % 8 == 0, "segments start on polyphase-group boundaries");
+static_assert(4 * 320 <= XBUF, "resampler staging fits the exchange buffer");
+static_assert((WARM - 12) % 4 == 0, "16-byte aligned tap reads");
+static_assert(WARM - 12 + 8 * ((TILE - WARM) * 5 / 8 / 5 - 1) + 32 <= TILE + TILE_PAD, "tap reads stay in the pad");
+
+// One wave resamples 64 consecutive groups (320 outputs) per step; the outputs are staged in
+// the wave's slice of the (then idle) exchange buffer and leave as aligned float4 stores.
+constexpr int RS_STAGE = 320;
+__device__ __forceinline__ void resample_tile(const float *__restrict__ tile, int64_t o_lo, int64_t o_hi,
+                                              float *__restrict__ yrow, float *__restrict__ stage, int lane,
+                                              int wave) {
+  const int ngrp = (int)((o_hi - o_lo + 4) / 5);
+  for (int j0 = 64 * wave; j0 < ngrp; j0 += 64 * (PT / 64)) {
+    const int j = j0 + lane;
+    if (j < ngrp) {
+      const float4 *x4 = reinterpret_cast<const float4 *>(tile + (WARM - 12) + 8 * j);
+      float v[32];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float4 f = x4[q];
+        v[4 * q] = f.x;
+        v[4 * q + 1] = f.y;
+        v[4 * q + 2] = f.z;
+        v[4 * q + 3] = f.w;
+      }
+#pragma unroll
+      for (int jj = 0; jj < 5; ++jj) {
+        float acc = 0.f;
+#pragma unroll
+        for (int t = 0; t < 28; ++t) acc = fmaf(kRs16k10k[jj][t], v[t + 2], acc);
+        // phase-major staging (output 5*lane + jj at jj*64 + lane): conflict-free, and no
+        // adjacent stores for the SLP vectorizer to pair into SGPR-literal packed FMAs
+        stage[64 * jj + lane] = acc;
+      }
+    }
+    wave_lds_fence();
+    const int64_t ob = o_lo + 5 * (int64_t)j0;  // multiple of 4: aligned float4 stores
+    const int n = (int)min((int64_t)RS_STAGE, o_hi - ob);
+    auto at = [&](int c) { return stage[64 * (c % 5) + c / 5]; };
+    for (int q = lane; 4 * q < n; q += 64) {
+      if (4 * q + 3 < n) {
+        reinterpret_cast<float4 *>(yrow + ob)[q] = make_float4(at(4 * q), at(4 * q + 1), at(4 * q + 2), at(4 * q + 3));
+      } else {
+        for (int c = 4 * q; c < n; ++c) yrow[ob + c] = at(c);
+      }
+    }
+    wave_lds_fence();
+  }
+}
+
 // Persistent: each workgroup walks items (signal, segment) = blockIdx.x, +gridDim.x, ...;
 // the next item's tile is in flight in registers while the current one is processed.
+template <bool JOINT, bool VARLEN>
 __global__ void __launch_bounds__(PT, 2)
     pesq_front(const float *__restrict__ ref, const float *__restrict__ deg, int64_t B, int64_t Lcap,
-               int64_t ld, const int32_t *__restrict__ lens, int F, int nseg, int64_t nitems,
-               float *__restrict__ bark, float *__restrict__ ppart) {
-  __shared__ __attribute__((aligned(16))) float tile[TILE];
+               int64_t ld, const int32_t *__restrict__ lens_arg, int F, int npseg, int nseg, int64_t nitems,
+               float *__restrict__ bark, float *__restrict__ ppart, float *__restrict__ y10, int64_t y_ld) {
+  __shared__ __attribute__((aligned(16))) float tile[TILE + TILE_PAD];
   __shared__ __attribute__((aligned(16))) float xbuf[XBUF];
   __shared__ float red[8];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int32_t *__restrict__ lens = VARLEN ? lens_arg : nullptr;  // uniform batches: no per-row lookups
+  if (JOINT && tid < TILE_PAD) tile[TILE + tid] = 0.f;  // never rewritten
   // ---- per-lane constants, loaded once
   float win[8];
   cf tw1[8], tw2[8];
@@ -250,8 +311,15 @@ __global__ void __launch_bounds__(PT, 2)
   for (; item < nitems; item += gridDim.x) {
     const Item it = make_item(item, nseg, B, ld, Lcap, lens, ref, deg);
     const int64_t L = it.L;
-    const Geometry rg = geometry(L);  // this row's geometry (== the launch's without lengths)
-    if (it.g >= rg.nseg) {  // segment past this row's end: no samples, no frames
+    Geometry rg;  // this row's geometry (the launch's for uniform batches)
+    if (VARLEN) {
+      rg = geometry(L);
+    } else {
+      rg.F = F;
+      rg.npseg = npseg;
+      rg.nseg = nseg;
+    }
+    if (VARLEN && it.g >= rg.nseg) {  // segment past this row's end: no samples, no frames
       if (tid == 0) ppart[it.s * nseg + it.g] = 0.f;
       const int64_t nxt = item + gridDim.x;
       if (nxt < nitems) prefetch(make_item(nxt, nseg, B, ld, Lcap, lens, ref, deg), tid, pre);
@@ -260,10 +328,34 @@ __global__ void __launch_bounds__(PT, 2)
     STAMP(0);
     {
       float4 *t4 = reinterpret_cast<float4 *>(tile);
+      if (JOINT && it.tstart + TILE > L) {  // the row ends in this tile: the resampler sees zeros
+#pragma unroll                               // past it (torchaudio pads, base.py:20)
+        for (int k = 0; k < PF; ++k) {
+          float4 v = pre[k];
+          const int t = (int)(it.tstart - (L & ~(int64_t)3)) + 4 * (tid + PT * k);  // vs ceil4 start
+          if (t >= 0) {
+            const int r = (int)(L & 3);  // valid samples in the float4 that starts at floor4(L)
+            v.x = (t == 0 && r > 0) ? v.x : 0.f;
+            v.y = (t == 0 && r > 1) ? v.y : 0.f;
+            v.z = (t == 0 && r > 2) ? v.z : 0.f;
+            v.w = 0.f;
+          }
+          t4[tid + PT * k] = v;
+        }
+      } else {
 #pragma unroll
-      for (int k = 0; k < PF; ++k) t4[tid + PT * k] = pre[k];
+        for (int k = 0; k < PF; ++k) t4[tid + PT * k] = pre[k];
+      }
     }
     lds_barrier();
+    if (JOINT) {
+      const int64_t L10 = (5 * L + 7) / 8;
+      const int64_t o_lo = (int64_t)it.g * OWN10;
+      const int64_t o_hi = (it.g == rg.nseg - 1) ? L10 : min(L10, o_lo + OWN10);
+      const int64_t b = it.s < B ? it.s : it.s - B;
+      resample_tile(tile, o_lo, o_hi, y10 + (2 * b + (it.s < B ? 0 : 1)) * y_ld, xbuf + RS_STAGE * wave, lane,
+                    wave);
+    }
     STAMP(1);
     const int g = it.g;
     const int64_t tstart = it.tstart;
@@ -703,9 +795,9 @@ extern "C" size_t fsem_pesq_workspace_bytes(int64_t batch, int64_t length) {
   return bytes;
 }
 
-extern "C" int fsem_pesq_front_f32(const float *ref, const float *deg, int64_t batch, int64_t length,
-                                   int64_t ld, const int32_t *lengths, float *bark, float *power, void *ws,
-                                   size_t ws_bytes, void *stream) {
+int fsem::pesq::launch_front(const float *ref, const float *deg, int64_t batch, int64_t length, int64_t ld,
+                             const int32_t *lengths, float *bark, float *power, void *ws, size_t ws_bytes,
+                             float *y10, int64_t y_ld, hipStream_t st) {
   if (!ref || !deg || !bark || !power || batch <= 0 || length <= 0 || ld < length) return FSEM_EINVAL;
   const pesq::Geometry g = pesq::geometry(length);
   if (g.F < 20 && !lengths) return FSEM_ESHORT;
@@ -715,14 +807,29 @@ extern "C" int fsem_pesq_front_f32(const float *ref, const float *deg, int64_t b
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
   const int64_t grid = std::min<int64_t>(nitems, (int64_t)ncu * 2);  // 2 resident workgroups per CU
   float *ppart = static_cast<float *>(ws);
-  hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(pesq::pesq_front, dim3((unsigned)grid), dim3(pesq::PT), 0, st, ref, deg, batch,
-                     length, ld, lengths, g.F, g.nseg, nitems, bark, ppart);
+#define FSEM_FRONT(J, V)                                                                                \
+  hipLaunchKernelGGL((pesq::pesq_front<J, V>), dim3((unsigned)grid), dim3(pesq::PT), 0, st, ref, deg, batch, \
+                     length, ld, lengths, g.F, g.npseg, g.nseg, nitems, bark, ppart, y10, y_ld)
+  if (y10) {
+    if (lengths) FSEM_FRONT(true, true);
+    else FSEM_FRONT(true, false);
+  } else {
+    if (lengths) FSEM_FRONT(false, true);
+    else FSEM_FRONT(false, false);
+  }
+#undef FSEM_FRONT
   FSEM_CHECK_LAUNCH();
   hipLaunchKernelGGL(pesq::pesq_power_sum, dim3((unsigned)((2 * batch + 255) / 256)), dim3(256), 0, st,
                      ppart, g.nseg, 2 * batch, power);
   FSEM_CHECK_LAUNCH();
   return FSEM_OK;
+}
+
+extern "C" int fsem_pesq_front_f32(const float *ref, const float *deg, int64_t batch, int64_t length,
+                                   int64_t ld, const int32_t *lengths, float *bark, float *power, void *ws,
+                                   size_t ws_bytes, void *stream) {
+  return pesq::launch_front(ref, deg, batch, length, ld, lengths, bark, power, ws, ws_bytes, nullptr, 0,
+                            (hipStream_t)stream);
 }
 
 extern "C" size_t fsem_pesq_back_workspace_bytes(int64_t batch, int64_t length) {
@@ -744,9 +851,9 @@ extern "C" int fsem_pesq_back_f32(const float *bark, const float *power, int64_t
   return FSEM_OK;
 }
 
-extern "C" int fsem_pesq_wb_f32(const float *ref, const float *deg, int64_t batch, int64_t length,
-                                int64_t ld, const int32_t *lengths, float *mos, void *ws, size_t ws_bytes,
-                                void *stream) {
+int fsem::pesq::run_wb(const float *ref, const float *deg, int64_t batch, int64_t length, int64_t ld,
+                       const int32_t *lengths, float *mos, void *ws, size_t ws_bytes, float *y10, int64_t y_ld,
+                       hipStream_t stream) {
   if (!ref || !deg || !mos || batch <= 0 || length <= 0 || ld < length) return FSEM_EINVAL;
   const pesq::Geometry g = pesq::geometry(length);
   if (g.F < 20 && !lengths) return FSEM_ESHORT;
@@ -757,8 +864,14 @@ extern "C" int fsem_pesq_wb_f32(const float *ref, const float *deg, int64_t batc
   p += front + align_up(sizeof(float) * (size_t)(2 * batch) * (size_t)g.F * pesq::NBARK, 256);
   float *power = reinterpret_cast<float *>(p);
   p += align_up(sizeof(float) * (size_t)(2 * batch), 256);
-  int rc = fsem_pesq_front_f32(ref, deg, batch, length, ld, lengths, bark, power, ws, front, stream);
+  int rc = pesq::launch_front(ref, deg, batch, length, ld, lengths, bark, power, ws, front, y10, y_ld, stream);
   if (rc != FSEM_OK) return rc;
   return fsem_pesq_back_f32(bark, power, batch, length, lengths, mos, p,
                             fsem_pesq_back_workspace_bytes(batch, length), stream);
+}
+
+extern "C" int fsem_pesq_wb_f32(const float *ref, const float *deg, int64_t batch, int64_t length,
+                                int64_t ld, const int32_t *lengths, float *mos, void *ws, size_t ws_bytes,
+                                void *stream) {
+  return pesq::run_wb(ref, deg, batch, length, ld, lengths, mos, ws, ws_bytes, nullptr, 0, (hipStream_t)stream);
 }

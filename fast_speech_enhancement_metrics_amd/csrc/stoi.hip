@@ -18,7 +18,10 @@
 //  stoi_seg      per utterance: 30-frame segments -- equalisation + clipping, row / column
 //                normalisation and correlations for STOI and ESTOI (STOI.py:113-198), one
 //                lane per segment, band envelopes staged in LDS (no 30x materialisation).
+#include <algorithm>
+
 #include "fsem_fft.h"
+#include "fsem_internal.h"
 #include "fsem_resample.h"
 
 namespace fsem {
@@ -231,6 +234,32 @@ __global__ void __launch_bounds__(256)
       }
     }
     lds_barrier();
+  }
+}
+
+// Joint mode: the 10 kHz rows were written by pesq_front<true>; clean frame energies
+// (STOI.py:92-99) from them, one wave per frame, same arithmetic order as the fused kernels.
+constexpr int VFE = 64;  // VAD frames per workgroup
+__global__ void __launch_bounds__(256)
+    stoi_vad10(const float *__restrict__ y10, int64_t y_ld, Rows rows, float *__restrict__ energy, int nv_ld) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t b = blockIdx.y;
+  const int NV = rows.nv(b);
+  const float *__restrict__ yc = y10 + (2 * b) * y_ld;
+  const float w0 = kHann256s[lane], w1 = kHann256s[lane + 64], w2 = kHann256s[lane + 128],
+              w3 = kHann256s[lane + 192];
+  for (int f = wave; f < VFE; f += 4) {
+    const int i = blockIdx.x * VFE + f;
+    if (i >= NV) break;
+    const float *fr = yc + 128 * (int64_t)i;
+    const float v0 = w0 * fr[lane], v1 = w1 * fr[lane + 64], v2 = w2 * fr[lane + 128], v3 = w3 * fr[lane + 192];
+    float acc = 0.f;
+    acc = fmaf(v0, v0, acc);
+    acc = fmaf(v1, v1, acc);
+    acc = fmaf(v2, v2, acc);
+    acc = fmaf(v3, v3, acc);
+    acc = wave_sum(acc);
+    if (lane == 0) energy[b * nv_ld + i] = 20.f * log10f(sqrtf(acc) + 1e-9f);
   }
 }
 
@@ -537,46 +566,31 @@ inline size_t ws_bytes(int64_t B, const Geometry &g) {
   return s;
 }
 
-inline int run(const float *ref, const float *deg, int64_t B, int64_t length, int64_t ld,
-               const int32_t *lengths, int32_t sr, float *stoi_out, float *estoi_out, int32_t *kept_out,
-               float *tob_out, int64_t tob_ld, void *ws, size_t ws_size, hipStream_t st) {
-  Geometry g;
-  ResampleKernel rk;
-  int rc = make_geometry(length, sr, &g, &rk);
-  if (rc != FSEM_OK) return rc;
-  if (g.NV <= 0 && !lengths) return FSEM_ESHORT;  // with lengths: NaN rows instead
-  const Rows rows{lengths, length, rk.orig, rk.nw};
-  if (!ws || ws_size < ws_bytes(B, g)) return FSEM_EWORKSPACE;
-  if (B > 65535) return FSEM_EINVAL;
+// Pointers into a STOI workspace laid out by ws_bytes().
+struct Ws {
+  float *energy;
+  int *idx, *kept;
+  float *tob, *y10;
+};
+
+inline Ws carve(void *ws, int64_t B, const Geometry &g) {
+  Ws w;
   char *p = static_cast<char *>(ws);
-  float *energy = reinterpret_cast<float *>(p);
+  w.energy = reinterpret_cast<float *>(p);
   p += align_up(sizeof(float) * (size_t)B * g.nv_ld, 256);
-  int *idx = reinterpret_cast<int *>(p);
+  w.idx = reinterpret_cast<int *>(p);
   p += align_up(sizeof(int) * (size_t)B * g.nv_ld, 256);
-  int *kept = reinterpret_cast<int *>(p);
+  w.kept = reinterpret_cast<int *>(p);
   p += align_up(sizeof(int) * (size_t)B, 256);
-  float *tob = reinterpret_cast<float *>(p);
-  int64_t tmax = g.tmax;
-  if (tob_out) {
-    tob = tob_out;
-    tmax = tob_ld;
-  }
-  if (kept_out) kept = kept_out;
-  float *y10 = reinterpret_cast<float *>(reinterpret_cast<char *>(ws) + ws_bytes(B, g) -
-                                         align_up(sizeof(float) * (size_t)(2 * B) * (size_t)g.y_ld, 256));
-  if (g.mode == 0) {
-    const int nchunk = (int)((g.L10 + VF2 * 128 - 1) / (VF2 * 128));
-    const int64_t nitems = B * (int64_t)nchunk * 2;
-    int dev = 0, ncu = 256;
-    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    const int64_t grid = nitems < (int64_t)ncu * 3 ? nitems : (int64_t)ncu * 3;  // 3 resident per CU
-    hipLaunchKernelGGL(stoi_resample_vad16, dim3((unsigned)grid), dim3(256), 0, st, ref, deg, rows, ld, nchunk,
-                       nitems, y10, g.y_ld, energy, g.nv_ld);
-  } else {
-    hipLaunchKernelGGL(stoi_resample_vad, dim3((unsigned)((g.L10 + VF3 * 128 - 1) / (VF3 * 128)), (unsigned)B),
-                       dim3(256), 0, st, ref, deg, rows, ld, g.mode, rk, y10, g.y_ld, energy, g.nv_ld);
-  }
-  FSEM_CHECK_LAUNCH();
+  w.tob = reinterpret_cast<float *>(p);
+  w.y10 = reinterpret_cast<float *>(static_cast<char *>(ws) + ws_bytes(B, g) -
+                                    align_up(sizeof(float) * (size_t)(2 * B) * (size_t)g.y_ld, 256));
+  return w;
+}
+
+// Everything after the clean frame energies: selection, band envelopes, segments.
+inline int run_tail(int64_t B, const Geometry &g, const Rows &rows, const float *y10, const float *energy, int *idx,
+                    int *kept, float *tob, int64_t tmax, float *stoi_out, float *estoi_out, hipStream_t st) {
   hipLaunchKernelGGL(stoi_select, dim3((unsigned)B), dim3(256), 0, st, energy, g.nv_ld, rows, idx, kept);
   FSEM_CHECK_LAUNCH();
   hipLaunchKernelGGL(stoi_tob, dim3((unsigned)((g.tmax + TF - 1) / TF), (unsigned)B), dim3(256), 0, st, y10,
@@ -588,6 +602,40 @@ inline int run(const float *ref, const float *deg, int64_t B, int64_t length, in
     FSEM_CHECK_LAUNCH();
   }
   return FSEM_OK;
+}
+
+inline int run(const float *ref, const float *deg, int64_t B, int64_t length, int64_t ld,
+               const int32_t *lengths, int32_t sr, float *stoi_out, float *estoi_out, int32_t *kept_out,
+               float *tob_out, int64_t tob_ld, void *ws, size_t ws_size, hipStream_t st) {
+  Geometry g;
+  ResampleKernel rk;
+  int rc = make_geometry(length, sr, &g, &rk);
+  if (rc != FSEM_OK) return rc;
+  if (g.NV <= 0 && !lengths) return FSEM_ESHORT;  // with lengths: NaN rows instead
+  const Rows rows{lengths, length, rk.orig, rk.nw};
+  if (!ws || ws_size < ws_bytes(B, g)) return FSEM_EWORKSPACE;
+  if (B > 65535) return FSEM_EINVAL;
+  Ws w = carve(ws, B, g);
+  int64_t tmax = g.tmax;
+  if (tob_out) {
+    w.tob = tob_out;
+    tmax = tob_ld;
+  }
+  if (kept_out) w.kept = kept_out;
+  if (g.mode == 0) {
+    const int nchunk = (int)((g.L10 + VF2 * 128 - 1) / (VF2 * 128));
+    const int64_t nitems = B * (int64_t)nchunk * 2;
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const int64_t grid = nitems < (int64_t)ncu * 3 ? nitems : (int64_t)ncu * 3;  // 3 resident per CU
+    hipLaunchKernelGGL(stoi_resample_vad16, dim3((unsigned)grid), dim3(256), 0, st, ref, deg, rows, ld, nchunk,
+                       nitems, w.y10, g.y_ld, w.energy, g.nv_ld);
+  } else {
+    hipLaunchKernelGGL(stoi_resample_vad, dim3((unsigned)((g.L10 + VF3 * 128 - 1) / (VF3 * 128)), (unsigned)B),
+                       dim3(256), 0, st, ref, deg, rows, ld, g.mode, rk, w.y10, g.y_ld, w.energy, g.nv_ld);
+  }
+  FSEM_CHECK_LAUNCH();
+  return run_tail(B, g, rows, w.y10, w.energy, w.idx, w.kept, w.tob, tmax, stoi_out, estoi_out, st);
 }
 
 }  // namespace stoi
@@ -621,6 +669,35 @@ extern "C" int fsem_stoi_tob_f32(const float *ref10, const float *deg10, int64_t
   if (tmax < g.tmax) return FSEM_EINVAL;
   return stoi::run(ref10, deg10, batch, length10, ld, nullptr, 10000, nullptr, nullptr, kept, tob, tmax, ws,
                    ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" size_t fsem_pesq_stoi_workspace_bytes(int64_t batch, int64_t length) {
+  return align_up(fsem_pesq_workspace_bytes(batch, length), 256) + fsem_stoi_workspace_bytes(batch, length, 16000);
+}
+
+extern "C" int fsem_pesq_stoi_f32(const float *ref, const float *deg, int64_t batch, int64_t length, int64_t ld,
+                                  const int32_t *lengths, float *mos, float *stoi_out, float *estoi_out, void *ws,
+                                  size_t ws_bytes, void *stream) {
+  if (!ref || !deg || !mos || !stoi_out || !estoi_out || batch <= 0 || length <= 0 || ld < length)
+    return FSEM_EINVAL;
+  if (batch > 65535) return FSEM_EINVAL;
+  stoi::Geometry g;
+  ResampleKernel rk;
+  int rc = stoi::make_geometry(length, 16000, &g, &rk);
+  if (rc != FSEM_OK) return rc;
+  if (!lengths && (g.NV <= 0 || fsem_pesq_frames(length) < 20)) return FSEM_ESHORT;
+  if (!ws || ws_bytes < fsem_pesq_stoi_workspace_bytes(batch, length)) return FSEM_EWORKSPACE;
+  const size_t pesq_bytes = align_up(fsem_pesq_workspace_bytes(batch, length), 256);
+  stoi::Ws w = stoi::carve(static_cast<char *>(ws) + pesq_bytes, batch, g);
+  const stoi::Rows rows{lengths, length, rk.orig, rk.nw};
+  hipStream_t st = (hipStream_t)stream;
+  // PESQ-wb with the 10 kHz rows emitted from the same input tiles
+  rc = pesq::run_wb(ref, deg, batch, length, ld, lengths, mos, ws, pesq_bytes, w.y10, g.y_ld, st);
+  if (rc != FSEM_OK) return rc;
+  hipLaunchKernelGGL(stoi::stoi_vad10, dim3((unsigned)std::max(1, (g.NV + stoi::VFE - 1) / stoi::VFE), (unsigned)batch),
+                     dim3(256), 0, st, w.y10, g.y_ld, rows, w.energy, g.nv_ld);
+  FSEM_CHECK_LAUNCH();
+  return stoi::run_tail(batch, g, rows, w.y10, w.energy, w.idx, w.kept, w.tob, g.tmax, stoi_out, estoi_out, st);
 }
 
 extern "C" const char *fsem_strerror(int code) {

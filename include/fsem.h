@@ -115,6 +115,21 @@ int fsem_stoi_tob_f32(const float *ref10, const float *deg10, int64_t batch,
                       int64_t length10, int64_t ld, int32_t *kept, float *tob, int64_t tmax,
                       void *ws, size_t ws_bytes, void *stream);
 
+/* ---------------------------------------------------------------- joint PESQ + STOI
+ * Both metrics of 16 kHz pairs from ONE read of the inputs: replaces the
+ * reference's two calls PESQ(16000).compute_metric (PESQ.py:232-245) and
+ * STOI(16000)(...) (base.py:19-20 resampling + STOI.py:153-205).  The PESQ front end's LDS
+ * tiles also feed the fused 16 -> 10 kHz resampler.  Scores are bitwise those of
+ * fsem_pesq_wb_f32 and fsem_stoi_f32(sample_rate = 16000) on the same rows.
+ *   lengths : NULL or [batch] int32 per-row lengths (Conventions)
+ *   mos, stoi, estoi : [batch] float32 outputs
+ * FSEM_ESHORT (whole-batch form) when either metric's minimum length is not met.
+ */
+size_t fsem_pesq_stoi_workspace_bytes(int64_t batch, int64_t length);
+int fsem_pesq_stoi_f32(const float *ref, const float *deg, int64_t batch, int64_t length,
+                       int64_t ld, const int32_t *lengths, float *mos, float *stoi, float *estoi,
+                       void *ws, size_t ws_bytes, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -177,3 +177,49 @@ def test_gpu_varlen_large_mixed_batch():
         s1, e1 = (t.item() for t in s.scores(c[b:b + 1, :n].contiguous(), d[b:b + 1, :n].contiguous(), 16000))
         assert abs(mos[b] - m1) < 1e-4, (b, mos[b], m1)
         assert abs(st[b] - s1) < 1e-5 and abs(es[b] - e1) < 1e-5, (b, st[b], s1)
+
+
+# ------------------------------------------------------------------------------- joint entry
+def test_joint_cpu_mode_matches_reference():
+    from fast_speech_enhancement_metrics_amd import PESQ_STOI
+    g = load_golden("varlen_16k")
+    c, d, lens = torch.from_numpy(g["clean_f"]), torch.from_numpy(g["noisy_f"]), g["lengths"]
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        res = PESQ_STOI(16000)(c, d, lengths=lens)
+    assert [sorted(r) for r in res] == [["ESTOI", "PESQ", "STOI"]] * len(lens)
+    _close_with_nans([r["PESQ"] for r in res], g["pesq"], 2e-3)
+    _close_with_nans([r["STOI"] for r in res], g["stoi"], 1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["pesq_ragged", "stoi_16k_10s", "varlen_16k"])
+def test_gpu_joint_bitwise_equals_separate_calls(name):
+    """fsem_pesq_stoi_f32 (one read of the inputs) == fsem_pesq_wb_f32 + fsem_stoi_f32, bitwise."""
+    from fast_speech_enhancement_metrics_amd import PESQ, PESQ_STOI, STOI
+    g = load_golden(name)
+    c = torch.from_numpy(g["clean_f"]).cuda()
+    d = torch.from_numpy(g["noisy_f"]).cuda()
+    lens = torch.from_numpy(g["lengths"]) if "lengths" in g else None
+    mos, s, e = PESQ_STOI(16000, use_gpu=True).scores(c, d, lens)
+    mos1 = PESQ(16000, use_gpu=True).scores(c, d, lens)
+    s1, e1 = STOI(16000, use_gpu=True).scores(c, d, 16000, lengths=lens)
+    assert torch.equal(mos, mos1, ) or torch.allclose(mos, mos1, atol=0, rtol=0, equal_nan=True)
+    assert torch.allclose(s, s1, atol=0, rtol=0, equal_nan=True)
+    assert torch.allclose(e, e1, atol=0, rtol=0, equal_nan=True)
+    if "pesq" in g and "lengths" in g:
+        _close_with_nans(mos.cpu().numpy(), g["pesq"], PESQ_TOL)
+        _close_with_nans(s.cpu().numpy(), g["stoi"], STOI_TOL)
+
+
+@pytest.mark.gpu
+def test_gpu_joint_api_list_of_dicts():
+    from fast_speech_enhancement_metrics_amd import PESQ_STOI
+    g = load_golden("varlen_16k")
+    lens = g["lengths"]
+    cl = [torch.from_numpy(g["clean_f"][b, :n]) for b, n in enumerate(lens)]
+    dl = [torch.from_numpy(g["noisy_f"][b, :n]) for b, n in enumerate(lens)]
+    res = PESQ_STOI(16000, use_gpu=True)(cl, dl)
+    _close_with_nans([r["PESQ"] for r in res], g["pesq"], PESQ_TOL)
+    _close_with_nans([r["STOI"] for r in res], g["stoi"], STOI_TOL)
+    _close_with_nans([r["ESTOI"] for r in res], g["estoi"], STOI_TOL)

@@ -43,9 +43,12 @@ def timeit(fn):
     return s.elapsed_time(e) / a.reps
 
 
+from fast_speech_enhancement_metrics_amd import PESQ_STOI  # noqa: E402
 p, st = PESQ(16000, use_gpu=True), STOI(16000, use_gpu=True)
+jt = PESQ_STOI(16000, use_gpu=True) if hasattr(lib, "fsem_pesq_stoi_f32") else None
+t_joint = timeit(lambda: jt.scores(c, n)) if jt is not None else float("nan")
 t_front = timeit(front)
 t_pesq = timeit(lambda: p.scores(c, n))
 t_stoi = timeit(lambda: st.scores(c, n, 16000))
 mos = p.scores(c, n)[:4].tolist()
-print(f"{os.path.basename(_native.LIB_PATH)}: pesq_front {t_front:.3f} ms  PESQ {t_pesq:.3f} ms  STOI {t_stoi:.3f} ms  mos[:4] {mos}")
+print(f"{os.path.basename(_native.LIB_PATH)}: pesq_front {t_front:.3f} ms  PESQ {t_pesq:.3f} ms  STOI {t_stoi:.3f} ms  joint {t_joint:.3f} ms  mos[:4] {mos}")
