@@ -5,16 +5,17 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-One step = the engine work behind the drop-in API calls ``PESQ(16000, use_gpu=True)`` and
-``STOI(16000, use_gpu=True)`` on this rank's batch (4096 pairs per GPU by default:
-BASELINE.json configs[1], 10 s @ 16 kHz fp32): ``PESQ.scores`` + ``STOI.scores`` (the same
-kernels ``__call__`` runs), the RCCL all-gather of the per-utterance [B, 3] scores over xGMI
+One step = PESQ-wb + STOI/ESTOI scores of this rank's batch (4096 pairs per GPU by default:
+BASELINE.json configs[1], 10 s @ 16 kHz fp32) through the fused joint entry
+``PESQ_STOI(16000, use_gpu=True).scores`` (fsem_pesq_stoi_f32: one read of the inputs, scores
+bitwise equal to the two separate API calls; ``--separate`` runs ``PESQ.scores`` +
+``STOI.scores`` instead), the RCCL all-gather of the per-utterance [B, 3] scores over xGMI
 (N > 1), and one device->host copy of the job's scores on rank 0.  The API's Python
 list-of-dict formatting is not included (see DESIGN.md for its cost).
 Weak scaling: every rank owns its own shard of utterances, generated in HBM before timing.
 
 Rank 0 prints ONE JSON line with the metric, the roofline of the dominant kernel
-(pesq_front: algorithmic bytes / its HIP-event-timed duration vs 8 TB/s) and the CPU
+(pesq_front<joint>: algorithmic bytes / its HIP-event-timed duration vs 8 TB/s) and the CPU
 baseline (the oracle CPU restatement on a bounded sample, single core).
 """
 from __future__ import annotations
@@ -44,6 +45,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=5)
+    ap.add_argument("--separate", action="store_true", help="two API calls (PESQ, STOI) instead of the joint entry")
     return ap.parse_args()
 
 
@@ -81,8 +83,9 @@ def cpu_baseline(clean, noisy, budget_s):
                       f"oracle numpy/C restatement, {dt:.1f} s"}
 
 
-def kernel_roofline(pesq, clean, noisy, reps):
-    """HIP-event timing of the dominant kernel (pesq_front via fsem_pesq_front_f32) on the
+def kernel_roofline(clean, noisy, reps, joint):
+    """HIP-event timing of the dominant kernel -- pesq_front, launched alone through its stage
+    entry (fsem_pesq_front_y10_f32 for the joint path, fsem_pesq_front_f32 otherwise) -- on the
     stream it is launched on; achieved = algorithmic bytes per launch / avg duration."""
     from fast_speech_enhancement_metrics_amd import _native
     lib = _native.load()
@@ -94,10 +97,17 @@ def kernel_roofline(pesq, clean, noisy, reps):
     ws = _native.workspace(lib.fsem_pesq_front_workspace_bytes(B, L), dev)
     stream = torch.cuda.current_stream(dev)
     h = stream.cuda_stream
+    y_ld = ((5 * L + 7) // 8 + 63) // 64 * 64
+    y10 = torch.empty(2 * B, y_ld, device=dev) if joint else None
 
     def launch():
-        _native.check(lib.fsem_pesq_front_f32(clean.data_ptr(), noisy.data_ptr(), B, L, L, None, bark.data_ptr(),
-                                              power.data_ptr(), ws.data_ptr(), ws.numel(), h), "front")
+        if joint:
+            rc = lib.fsem_pesq_front_y10_f32(clean.data_ptr(), noisy.data_ptr(), B, L, L, None, bark.data_ptr(),
+                                             power.data_ptr(), y10.data_ptr(), y_ld, ws.data_ptr(), ws.numel(), h)
+        else:
+            rc = lib.fsem_pesq_front_f32(clean.data_ptr(), noisy.data_ptr(), B, L, L, None, bark.data_ptr(),
+                                         power.data_ptr(), ws.data_ptr(), ws.numel(), h)
+        _native.check(rc, "front")
 
     launch()
     torch.cuda.synchronize(dev)
@@ -110,7 +120,7 @@ def kernel_roofline(pesq, clean, noisy, reps):
     ms = start.elapsed_time(end) / reps
     algo_bytes = 2 * B * L * 4  # both signals read once (2*L*4 B per pair)
     achieved = algo_bytes / (ms * 1e-3) / 1e9
-    return {"kernel": "pesq_front", "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+    return {"kernel": "pesq_front<joint>" if joint else "pesq_front", "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
             "ms_per_launch": round(ms, 4), "algorithmic_bytes_per_launch": algo_bytes}
 
@@ -128,7 +138,7 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    from fast_speech_enhancement_metrics_amd import PESQ, STOI
+    from fast_speech_enhancement_metrics_amd import PESQ, PESQ_STOI, STOI
     from fast_speech_enhancement_metrics_amd.synthetic import speech_like_pairs
 
     B, L = args.batch, args.length
@@ -136,13 +146,17 @@ def main():
     torch.cuda.synchronize(dev)
     pesq = PESQ(16000, use_gpu=True)
     stoi = STOI(16000, use_gpu=True)
+    joint = PESQ_STOI(16000, use_gpu=True)
 
     from fast_speech_enhancement_metrics_amd.distributed import gather_scores
 
     def step():
         # per-rank engine work: PESQ-wb and STOI/ESTOI scores of this rank's 4096 pairs
-        p = pesq.scores(clean, noisy)
-        s, e = stoi.scores(clean, noisy, 16000)
+        if args.separate:
+            p = pesq.scores(clean, noisy)
+            s, e = stoi.scores(clean, noisy, 16000)
+        else:
+            p, s, e = joint.scores(clean, noisy)
         local = torch.stack([p, s, e], dim=1)
         full = gather_scores(local, world * B) if distributed else local  # RCCL all-gather (xGMI)
         return full.cpu() if rank == 0 else None  # one device->host copy of the job's scores
@@ -168,7 +182,7 @@ def main():
     ms_per_step = dt / args.steps * 1e3
     value = world * B * args.steps / dt
 
-    roof = kernel_roofline(pesq, clean, noisy, args.kernel_reps)
+    roof = kernel_roofline(clean, noisy, args.kernel_reps, joint=not args.separate)
     out = None
     if rank == 0:
         cpu = None
@@ -179,7 +193,9 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (speech-like harmonic source + AM noise, SNR U[-5,25] dB, int16 grid)",
-            "config": {"workload": "PESQ-wb + STOI/ESTOI scores of 10 s @ 16 kHz fp32 pairs (engine path of the drop-in API)",
+            "config": {"workload": ("PESQ-wb + STOI/ESTOI scores of 10 s @ 16 kHz fp32 pairs, "
+                                    + ("two API calls (PESQ.scores + STOI.scores)" if args.separate else
+                                       "fused joint entry PESQ_STOI.scores (one read of the inputs)")),
                        "batch_per_gpu": B, "global_batch": world * B, "length": L, "sample_rate": 16000,
                        "parallelism": f"dp{world} (utterance shards, RCCL all-gather of scores)"},
             "roofline": roof, "cpu_baseline": cpu,

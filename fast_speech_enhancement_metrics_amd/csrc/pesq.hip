@@ -832,6 +832,14 @@ extern "C" int fsem_pesq_front_f32(const float *ref, const float *deg, int64_t b
                             (hipStream_t)stream);
 }
 
+extern "C" int fsem_pesq_front_y10_f32(const float *ref, const float *deg, int64_t batch, int64_t length,
+                                       int64_t ld, const int32_t *lengths, float *bark, float *power, float *y10,
+                                       int64_t y_ld, void *ws, size_t ws_bytes, void *stream) {
+  if (!y10 || y_ld < (5 * length + 7) / 8 || (y_ld & 3)) return FSEM_EINVAL;
+  return pesq::launch_front(ref, deg, batch, length, ld, lengths, bark, power, ws, ws_bytes, y10, y_ld,
+                            (hipStream_t)stream);
+}
+
 extern "C" size_t fsem_pesq_back_workspace_bytes(int64_t batch, int64_t length) {
   const pesq::Geometry g = pesq::geometry(length);
   return align_up(sizeof(float) * (size_t)batch * (size_t)g.F * 4, 256);

@@ -452,12 +452,14 @@ __global__ void __launch_bounds__(SEG_T)
           sx += x[t];
           sy += y[t];
         }
-        // equalize_clip (STOI.py:129-139)
-        const float alpha = sqrtf(sx2) / (sqrtf(sy2) + 1e-9f);
+        // equalize_clip (STOI.py:129-139).  Hardware sqrt / rcp / rsq (~1 ulp) instead of the
+        // correctly rounded sequences: ~1e-7 relative per segment, far inside the tolerance.
+        const float alpha = __builtin_amdgcn_sqrtf(sx2) * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(sy2) + 1e-9f);
         float syc = 0.f;
 #pragma unroll
         for (int t = 0; t < NSEG; ++t) syc += fminf(alpha * y[t], x[t] * kClip);
-        const float mx = sx / NSEG, my = sy / NSEG, myc = syc / NSEG;
+        constexpr float kInvN = 1.f / NSEG;
+        const float mx = sx * kInvN, my = sy * kInvN, myc = syc * kInvN;
         float dxx = 0.f, dyy = 0.f, dcc = 0.f, dxc = 0.f;
 #pragma unroll
         for (int t = 0; t < NSEG; ++t) {
@@ -468,13 +470,15 @@ __global__ void __launch_bounds__(SEG_T)
           dcc = fmaf(dc, dc, dcc);
           dxc = fmaf(dx, dc, dxc);
         }
-        const float nx = sqrtf(dxx), ny = sqrtf(dyy), nc = sqrtf(dcc);
-        // normalize() (STOI.py:113-119); a zero-variance row normalises to 0 here
-        s_acc += (nx > 0.f && nc > 0.f) ? dxc / (nx * nc) : 0.f;
+        // 1 / ||row - mean||; normalize() (STOI.py:113-119): a zero-variance row normalises to 0
+        const float rxn = dxx > 0.f ? __builtin_amdgcn_rsqf(dxx) : 0.f;
+        const float ryn = dyy > 0.f ? __builtin_amdgcn_rsqf(dyy) : 0.f;
+        const float rcn = dcc > 0.f ? __builtin_amdgcn_rsqf(dcc) : 0.f;
+        s_acc = fmaf(dxc * rxn, rcn, s_acc);
         stat[0][j][tid] = mx;
-        stat[1][j][tid] = nx > 0.f ? 1.f / nx : 0.f;
+        stat[1][j][tid] = rxn;
         stat[2][j][tid] = my;
-        stat[3][j][tid] = ny > 0.f ? 1.f / ny : 0.f;
+        stat[3][j][tid] = ryn;
       }
       // ESTOI: time-normalised rows, then band (column) normalisation (STOI.py:178-181)
       float mux[NB], rx[NB], muy[NB], ry[NB];
@@ -496,8 +500,8 @@ __global__ void __launch_bounds__(SEG_T)
           ma += a[j];
           mc += c[j];
         }
-        ma /= NB;
-        mc /= NB;
+        ma *= 1.f / NB;
+        mc *= 1.f / NB;
         float aa = 0.f, cc = 0.f, ac = 0.f;
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
@@ -506,8 +510,9 @@ __global__ void __launch_bounds__(SEG_T)
           cc = fmaf(dc, dc, cc);
           ac = fmaf(da, dc, ac);
         }
-        const float na = sqrtf(aa), nc = sqrtf(cc);
-        e_acc += (na > 0.f && nc > 0.f) ? ac / (na * nc) : 0.f;
+        const float ra = aa > 0.f ? __builtin_amdgcn_rsqf(aa) : 0.f;
+        const float rc = cc > 0.f ? __builtin_amdgcn_rsqf(cc) : 0.f;
+        e_acc = fmaf(ac * ra, rc, e_acc);
       }
       st += (double)s_acc;
       et += (double)e_acc;

@@ -223,3 +223,40 @@ def test_gpu_joint_api_list_of_dicts():
     _close_with_nans([r["PESQ"] for r in res], g["pesq"], PESQ_TOL)
     _close_with_nans([r["STOI"] for r in res], g["stoi"], STOI_TOL)
     _close_with_nans([r["ESTOI"] for r in res], g["estoi"], STOI_TOL)
+
+
+@pytest.mark.gpu
+def test_gpu_front_y10_resampler_and_front_unchanged():
+    """fsem_pesq_front_y10_f32: the 10 kHz rows match the reference's resampler (golden x10),
+    and bark / power are bitwise those of fsem_pesq_front_f32."""
+    from fast_speech_enhancement_metrics_amd import _native
+    lib = _native.load()
+    g = load_golden("stoi_16k")
+    dev = torch.device("cuda")
+    c = torch.from_numpy(g["clean_f"]).to(dev)
+    d = torch.from_numpy(g["noisy_f"]).to(dev)
+    B, L = c.shape
+    F = lib.fsem_pesq_frames(L)
+    L10 = (5 * L + 7) // 8
+    y_ld = (L10 + 63) // 64 * 64
+    outs = []
+    for joint in (False, True):
+        bark = torch.full((2 * B, F, 49), -1.0, device=dev)
+        power = torch.empty(2 * B, device=dev)
+        y10 = torch.full((2 * B, y_ld), float("nan"), device=dev)
+        ws = _native.workspace(lib.fsem_pesq_front_workspace_bytes(B, L), dev)
+        h = _native.stream_handle(dev)
+        if joint:
+            rc = lib.fsem_pesq_front_y10_f32(c.data_ptr(), d.data_ptr(), B, L, L, None, bark.data_ptr(),
+                                             power.data_ptr(), y10.data_ptr(), y_ld, ws.data_ptr(), ws.numel(), h)
+        else:
+            rc = lib.fsem_pesq_front_f32(c.data_ptr(), d.data_ptr(), B, L, L, None, bark.data_ptr(),
+                                         power.data_ptr(), ws.data_ptr(), ws.numel(), h)
+        _native.check(rc, "front")
+        outs.append((bark, power, y10))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    y = outs[1][2].cpu().numpy()
+    np.testing.assert_allclose(y[0::2, :L10], g["x10_clean"], atol=2e-6, rtol=0)
+    assert np.isfinite(y[1::2, :L10]).all()
+    assert lib.fsem_pesq_front_y10_f32(c.data_ptr(), d.data_ptr(), B, L, L, None, c.data_ptr(), c.data_ptr(),
+                                       c.data_ptr(), L10 - 1, c.data_ptr(), 1 << 30, None) == -1

@@ -1,0 +1,46 @@
+"""Per-kernel PMC summary of a tools/gpu_round.sh run (separate rocprofv3 --pmc passes).
+
+    python tools/pmc_summary.py gpurun_out/<tag> > profiles/<round>/pmc_summary.json
+
+Per fsem kernel, averaged over its launches: raw counter values, plus HBM bytes corrected as
+MI355X_MICROARCH.md 'HBM' prescribes: FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950
+FETCH_SIZE counts half the bytes of wide (16 B/lane) coalesced streaming reads, so
+hbm_read_bytes = 2 * 1024 * FETCH_SIZE; hbm_write_bytes = 1024 * WRITE_SIZE.
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def short(name: str) -> str:
+    base = name.split("(")[0].replace("void ", "")
+    return base
+
+
+def main(root: str):
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in glob.glob(os.path.join(root, "pmc_*", "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if "fsem" not in r["Kernel_Name"]:
+                continue
+            acc[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    out = {}
+    for k, counters in acc.items():
+        d = {c: sum(v) / len(v) for c, v in counters.items()}
+        d["launches"] = max(len(v) for v in counters.values())
+        if "FETCH_SIZE" in d:
+            d["hbm_read_bytes"] = 2 * 1024 * d["FETCH_SIZE"]
+        if "WRITE_SIZE" in d:
+            d["hbm_write_bytes"] = 1024 * d["WRITE_SIZE"]
+        if "hbm_read_bytes" in d and "hbm_write_bytes" in d:
+            d["hbm_bytes"] = d["hbm_read_bytes"] + d["hbm_write_bytes"]
+        out[k] = d
+    json.dump(out, sys.stdout, indent=1, sort_keys=True)
+    print()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
