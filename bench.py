@@ -109,7 +109,8 @@ def kernel_roofline(clean, noisy, reps, joint):
                                          power.data_ptr(), ws.data_ptr(), ws.numel(), h)
         _native.check(rc, "front")
 
-    launch()
+    for _ in range(3):  # steady state (clocks, TLB) as inside the timed steps
+        launch()
     torch.cuda.synchronize(dev)
     start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     start.record(stream)
@@ -120,9 +121,35 @@ def kernel_roofline(clean, noisy, reps, joint):
     ms = start.elapsed_time(end) / reps
     algo_bytes = 2 * B * L * 4  # both signals read once (2*L*4 B per pair)
     achieved = algo_bytes / (ms * 1e-3) / 1e9
+    traffic, source = pmc_traffic("pesq_front<true, false>" if joint else "pesq_front<false, false>", B, L)
     return {"kernel": "pesq_front<joint>" if joint else "pesq_front", "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-            "ms_per_launch": round(ms, 4), "algorithmic_bytes_per_launch": algo_bytes}
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "traffic_source": source, "ms_per_launch": round(ms, 4), "algorithmic_bytes_per_launch": algo_bytes}
+
+
+def pmc_traffic(kernel: str, B: int, L: int):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
+    (profiles/*/pmc_summary.json, tools/pmc_summary.py: FETCH_SIZE x2 gfx950 correction +
+    WRITE_SIZE, MI355X_MICROARCH.md 'HBM'), recorded at this same configuration; the counters
+    need their own rocprofv3 passes, so they cannot be read inside the timed run."""
+    import glob
+    if (B, L) != (4096, 160000):
+        return None, None
+    best = None
+    import re
+
+    def natural(path):  # profiles/r1_v10 after profiles/r1_v9
+        return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", path)]
+
+    for f in sorted(glob.glob(os.path.join(HERE, "profiles", "*", "pmc_summary.json")), key=natural):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        key = next((k for k in d if k.endswith(kernel)), None)
+        if key and "hbm_bytes" in d[key]:
+            best = (int(d[key]["hbm_bytes"]), os.path.relpath(f, HERE))
+    return best if best else (None, None)
 
 
 def main():

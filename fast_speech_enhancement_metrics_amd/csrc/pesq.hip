@@ -6,19 +6,21 @@
 //   Loudness                                   fast_se_metrics/utils/loudness.py:27-67
 // with two kernels:
 //
-// pesq_front  one 256-thread workgroup per (signal, segment of 56 frames):
-//   A  coalesced float4 load of a 15360-sample tile (768 warm-up + 56 hops + 1 hop) into LDS
+// pesq_front  persistent 256-thread workgroups over items (signal, segment of 48 frames):
+//   A  float4 buffer loads of a 13 312-sample tile (768 warm-up + 48 hops + 1 hop) into LDS,
+//      prefetched in registers during the previous item's FFT phase
+//   J  (joint entry only) STOI's 16 -> 10 kHz resampler on the same tile (see resample_tile)
 //   B  level-alignment band-pass power (PESQ.py:92-98), time-parallel:
-//        lane j owns chunk j (60 samples); end state of its zero-state response is a
-//        linear functional of the chunk (table kBpG); a 4-level Hillis-Steele scan with the
+//        lane j owns chunk j (52 samples); end state of its zero-state response is a
+//        linear functional of the chunk (table kScanG); a 4-level Hillis-Steele scan with the
 //        chunk transition powers (kBpScan) gives every lane its true start state; lane then
 //        re-runs the five-section cascade from that state and sums y^2 over the samples its
-//        segment owns.  Filter state decays to <1e-14 within 16 chunks, so 4 levels suffice.
+//        segment owns.  Filter state decays to <1e-11 within 16 chunks, so 4 levels suffice.
 //   C  taper of the first / last 15 samples (PESQ.py:108-109)
 //   D  pre-emphasis IIR (PESQ.py:111), same scan scheme (2 states), written back in place
 //   E  Hann-512 frames, two frames per 512-point complex FFT (z = frame_a + i*frame_b,
 //      radix-8 Stockham, one wave per FFT, LDS exchange), |X|^2 split, DC zeroed; the
-//      spectra of 16 frames are parked in the already-consumed part of the tile and the
+//      spectra of the 48 frames are parked in the already-consumed part of the tile and the
 //      Bark contraction fbank[49x256] x spec runs on MFMA (v_mfma_f32_16x16x4_f32) over the
 //      block-sparse K-steps of each 16-band tile.
 //   Outputs per signal: Bark bands [F, 49] BEFORE the level scale (linear, applied in the
@@ -54,7 +56,7 @@ __device__ unsigned long long g_stamps[kStampBlocks][16];
 
 constexpr int PT = 256;
 constexpr int CH = FSEM_PESQ_CH;  // 52 samples per lane (stride 208 B: conflict-free b128)
-constexpr int TILE = PT * CH;     // 15360
+constexpr int TILE = PT * CH;     // 13312
 constexpr int WARM = 768;
 constexpr int NF = 48;            // frames per segment
 constexpr int OWN = NF * 256;     // samples of band-pass power owned per segment
