@@ -27,6 +27,7 @@ import sys
 import time
 
 import torch
+import torch.distributed as dist
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
@@ -46,6 +47,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=5)
     ap.add_argument("--separate", action="store_true", help="two API calls (PESQ, STOI) instead of the joint entry")
+    ap.add_argument("--workload", default="c2", choices=["c2", "c5"],
+                    help="c2: BASELINE metric (default); c5: config 5, mixed 8/16 kHz ragged 2-30 s batch")
     return ap.parse_args()
 
 
@@ -152,6 +155,82 @@ def pmc_traffic(kernel: str, B: int, L: int):
     return best if best else (None, None)
 
 
+def run_c5(args, world, rank, dev, distributed):
+    """BASELINE.json configs[4] / SURVEY 8(d) C5: 2048 utterances per GPU (16384 on 8), lengths
+    uniform in 2-30 s, half at 8 kHz (PESQ via 8->16 kHz, STOI via 8->10 kHz, as the reference's
+    PESQ(8000) / STOI(8000)) and half at 16 kHz (joint entry); ragged rows with per-row lengths.
+    The global plan (lengths, rates) is seeded and identical on every rank; utterances go to
+    ranks by LPT over their 16 kHz-equivalent length (distributed.lpt_shards)."""
+    import numpy as np
+    from fast_speech_enhancement_metrics_amd import PESQ, PESQ_STOI, STOI
+    from fast_speech_enhancement_metrics_amd.batching import resampled_lengths
+    from fast_speech_enhancement_metrics_amd.distributed import lpt_shards
+    from fast_speech_enhancement_metrics_amd.resample import Resample
+    from fast_speech_enhancement_metrics_amd.synthetic import speech_like_pairs
+
+    n_total = 2048 * world
+    rng = np.random.default_rng(5)
+    secs = rng.uniform(2.0, 30.0, size=n_total)
+    rate = np.where(np.arange(n_total) % 2 == 0, 8000, 16000)
+    lens = np.round(secs * rate).astype(np.int64)
+    cost = np.where(rate == 8000, 2 * lens, lens)  # 16 kHz-equivalent samples
+    mine = np.array(lpt_shards(cost, world)[rank], dtype=np.int64)
+    groups = {}
+    for sr in (8000, 16000):
+        idx = mine[rate[mine] == sr]
+        ln = lens[idx]
+        cap = int(-(-int(ln.max()) // 4) * 4)
+        cs, ns = [], []
+        for lo in range(0, len(idx), 256):  # generate in slices (bounded temporaries)
+            c, n, _ = speech_like_pairs(min(256, len(idx) - lo), cap, sr, seed=1000 + 7 * rank + lo + sr, device=dev)
+            cs.append(c)
+            ns.append(n)
+        groups[sr] = (torch.cat(cs), torch.cat(ns), torch.from_numpy(ln.astype(np.int32)).to(dev))
+    joint = PESQ_STOI(16000, use_gpu=True)
+    p8, s8 = PESQ(8000, use_gpu=True), STOI(8000, use_gpu=True)
+    up = Resample(8000, 16000).to(dev)
+
+    def step():
+        c, n, l16 = groups[16000]
+        out16 = torch.stack(joint.scores(c, n, lengths=l16), 1)
+        c8, n8, l8 = groups[8000]
+        l8to16 = resampled_lengths(l8, 8000, 16000).to(dev)
+        mos8 = p8.scores(up(c8), up(n8), lengths=l8to16)
+        st8, es8 = s8.scores(c8, n8, 8000, lengths=l8)
+        out8 = torch.stack([mos8, st8, es8], 1)
+        res = torch.cat([out8, out16])
+        return res.cpu() if rank == 0 else None
+
+    for _ in range(args.warmup):
+        step()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    if distributed:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    if rank == 0:
+        audio_s = float(secs.sum())
+        print(json.dumps({
+            "metric": "utterances/sec PESQ+STOI, mixed 8/16 kHz, variable 2-30 s (config 5)",
+            "value": round(n_total * args.steps / dt, 2), "unit": "utterances/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic speech-like pairs, lengths U[2,30] s, half 8 kHz / half 16 kHz",
+            "config": {"workload": "config 5: ragged PESQ-wb (8 kHz via 8->16 kHz) + STOI/ESTOI, per-row lengths",
+                       "global_batch": n_total, "audio_seconds_per_step": round(audio_s, 1),
+                       "audio_seconds_per_sec": round(audio_s * args.steps / dt, 1),
+                       "parallelism": f"dp{world} (LPT shards by 16 kHz-equivalent length)"}}), flush=True)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -164,6 +243,12 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if args.workload == "c5":
+        run_c5(args, world, rank, dev, distributed)
+        if distributed:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
 
     from fast_speech_enhancement_metrics_amd import PESQ, PESQ_STOI, STOI
     from fast_speech_enhancement_metrics_amd.synthetic import speech_like_pairs

@@ -48,14 +48,139 @@ int make_resample_kernel(int32_t orig_freq, int32_t new_freq, ResampleKernel *rk
   return FSEM_OK;
 }
 
-__global__ void __launch_bounds__(256) resample_kernel(const float *__restrict__ in, int64_t n_in,
-                                                       int64_t ld_in, float *__restrict__ out,
-                                                       int64_t n_out, int64_t ld_out,
-                                                       ResampleKernel rk) {
-  const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// Tiled form: a workgroup owns gt consecutive polyphase groups m (group m = inputs
+// x[m*orig - width, +taps) -> outputs [m*nw, +nw)).  The input window and the [nw, taps]
+// coefficients are staged in LDS with coalesced loads (zeros outside the row: torchaudio's
+// padding), each thread evaluates one group, and the outputs leave through LDS as coalesced
+// stores.  Same tap order as resample_at (bitwise the same samples).
+constexpr int RS_T = 256;
+constexpr int RS_XS = 8192 + FSEM_RS_MAX_COEF;  // staged inputs: GT*orig + taps <= this
+__global__ void __launch_bounds__(RS_T) resample_tiled(const float *__restrict__ in, int64_t n_in, int64_t ld_in,
+                                                      const int32_t *__restrict__ lens, float *__restrict__ out,
+                                                      int64_t ld_out, int gt, ResampleKernel rk) {
+  __shared__ float xs[RS_XS];
+  __shared__ float ks[FSEM_RS_MAX_COEF];
+  __shared__ float ys[RS_T * 8];
+  const int tid = threadIdx.x;
   const int64_t r = blockIdx.y;
-  if (o >= n_out) return;
-  out[r * ld_out + o] = resample_at(in + r * ld_in, n_in, o, rk);
+  int64_t n = n_in;
+  if (lens) {
+    const int64_t v = lens[r];
+    n = v < 0 ? 0 : (v > n_in ? n_in : v);
+  }
+  const int orig = rk.orig, nw = rk.nw, taps = rk.taps;
+  const int64_t n_out = (n * nw + orig - 1) / orig;
+  const int64_t m0 = (int64_t)blockIdx.x * gt;
+  if (m0 * nw >= n_out) return;
+  const float *__restrict__ x = in + r * ld_in;
+  const int64_t base = m0 * orig - rk.width;
+  const int nx = (gt - 1) * orig + taps;
+  for (int i = tid; i < nx; i += RS_T) {
+    const int64_t t = base + i;
+    xs[i] = (t >= 0 && t < n) ? x[t] : 0.f;
+  }
+  for (int i = tid; i < nw * taps; i += RS_T) ks[i] = rk.k[i];
+  __syncthreads();
+  // groups in chunks whose outputs fit the staging buffer; thread tid evaluates groups
+  // g0 + tid, g0 + tid + RS_T, ...; outputs leave as coalesced stores
+  constexpr int YS = RS_T * 8;
+  const int gc = YS / nw;  // groups per chunk (nw <= FSEM_RS_MAX_COEF / taps < YS)
+  for (int g0 = 0; g0 < gt; g0 += gc) {
+    const int g1 = min(gt, g0 + gc);
+    if (g0) __syncthreads();
+    for (int g = g0 + tid; g < g1; g += RS_T) {
+      const float *xg = xs + g * orig;
+      for (int j = 0; j < nw; ++j) {
+        const float *kj = ks + j * taps;
+        float acc = 0.f;
+        for (int t = 0; t < taps; ++t) acc = fmaf(kj[t], xg[t], acc);
+        ys[(g - g0) * nw + j] = acc;
+      }
+    }
+    __syncthreads();
+    const int nc = (g1 - g0) * nw;
+    const int64_t ob = (m0 + g0) * nw;
+    for (int i = tid; i < nc; i += RS_T) {
+      if (ob + i < n_out) out[r * ld_out + ob + i] = ys[i];
+    }
+  }
+}
+
+// Specialisation for the common rate pairs (8 -> 16 kHz, 8 -> 10 kHz, 48 -> 16 kHz): each lane
+// keeps its group's taps in registers and takes the coefficients from the kernel argument
+// block by scalar loads (compile-time indices), so the inner loop is NW*TAPS register FMAs.
+template <int ORIG, int NW, int TAPS>
+__global__ void __launch_bounds__(RS_T) resample_tiled_t(const float *__restrict__ in, int64_t n_in, int64_t ld_in,
+                                                        const int32_t *__restrict__ lens, float *__restrict__ out,
+                                                        int64_t ld_out, int gt, ResampleKernel rk) {
+  __shared__ float xs[RS_XS];
+  __shared__ float ys[RS_T * 8];
+  const int tid = threadIdx.x;
+  const int64_t r = blockIdx.y;
+  int64_t n = n_in;
+  if (lens) {
+    const int64_t v = lens[r];
+    n = v < 0 ? 0 : (v > n_in ? n_in : v);
+  }
+  const int64_t n_out = (n * NW + ORIG - 1) / ORIG;
+  const int64_t m0 = (int64_t)blockIdx.x * gt;
+  if (m0 * NW >= n_out) return;
+  const float *__restrict__ x = in + r * ld_in;
+  const int64_t base = m0 * ORIG - rk.width;
+  const int nx = (gt - 1) * ORIG + TAPS;
+  for (int i = tid; i < nx; i += RS_T) {
+    const int64_t t = base + i;
+    xs[i] = (t >= 0 && t < n) ? x[t] : 0.f;
+  }
+  __syncthreads();
+  constexpr int GC = RS_T * 8 / NW / RS_T * RS_T;  // groups per chunk, a multiple of RS_T
+  static_assert(GC >= RS_T, "chunk holds one group per thread");
+  for (int g0 = 0; g0 < gt; g0 += GC) {
+    const int g1 = min(gt, g0 + GC);
+    if (g0) __syncthreads();
+    for (int g = g0 + tid; g < g1; g += RS_T) {
+      float v[TAPS];
+#pragma unroll
+      for (int t = 0; t < TAPS; ++t) v[t] = xs[g * ORIG + t];
+#pragma unroll
+      for (int j = 0; j < NW; ++j) {
+        float acc = 0.f;
+#pragma unroll
+        for (int t = 0; t < TAPS; ++t) acc = fmaf(rk.k[j * TAPS + t], v[t], acc);
+        ys[(g - g0) * NW + j] = acc;
+      }
+    }
+    __syncthreads();
+    const int nc = (g1 - g0) * NW;
+    const int64_t ob = (m0 + g0) * NW;
+    for (int i = tid; i < nc; i += RS_T) {
+      if (ob + i < n_out) out[r * ld_out + ob + i] = ys[i];
+    }
+  }
+}
+
+int launch_resample_tiled(const float *in, int64_t rows, int64_t n_in, int64_t ld_in, const int32_t *lens,
+                          float *out, int64_t ld_out, const ResampleKernel &rk, hipStream_t st) {
+  if (rows <= 0 || n_in <= 0) return FSEM_OK;
+  if (rows > 65535) return FSEM_EINVAL;
+  const int gt = (RS_XS - rk.taps) / rk.orig + 1;  // groups per workgroup (inputs staged once)
+  if (gt < 1 || rk.nw > RS_T * 8) return FSEM_ERATE;
+  const int64_t groups = (n_in + rk.orig - 1) / rk.orig + 1;
+  dim3 grid((unsigned)((groups + gt - 1) / gt), (unsigned)rows);
+#define FSEM_RS_CASE(O, N, T)                                                                                \
+  if (rk.orig == O && rk.nw == N && rk.taps == T) {                                                          \
+    hipLaunchKernelGGL((resample_tiled_t<O, N, T>), grid, dim3(RS_T), 0, st, in, n_in, ld_in, lens, out, ld_out, \
+                       gt, rk);                                                                               \
+    FSEM_CHECK_LAUNCH();                                                                                      \
+    return FSEM_OK;                                                                                           \
+  }
+  FSEM_RS_CASE(1, 2, 15)   // 8 -> 16 kHz (PESQ at 8 kHz)
+  FSEM_RS_CASE(4, 5, 18)   // 8 -> 10 kHz (STOI at 8 kHz)
+  FSEM_RS_CASE(3, 1, 41)   // 48 -> 16 kHz
+#undef FSEM_RS_CASE
+  hipLaunchKernelGGL(resample_tiled, grid, dim3(RS_T), 0, st, in, n_in, ld_in, lens, out, ld_out, gt, rk);
+  FSEM_CHECK_LAUNCH();
+  return FSEM_OK;
 }
 
 }  // namespace fsem
@@ -77,9 +202,5 @@ extern "C" int fsem_resample_f32(const float *in, int64_t rows, int64_t n_in, in
   if (rc != FSEM_OK) return rc;
   const int64_t n_out = (rk.nw * n_in + rk.orig - 1) / rk.orig;
   if (ld_out < n_out || rows > 65535) return FSEM_EINVAL;
-  dim3 grid((unsigned)((n_out + 255) / 256), (unsigned)rows);
-  hipLaunchKernelGGL(fsem::resample_kernel, grid, dim3(256), 0, (hipStream_t)stream, in, n_in,
-                     ld_in, out, n_out, ld_out, rk);
-  FSEM_CHECK_LAUNCH();
-  return FSEM_OK;
+  return fsem::launch_resample_tiled(in, rows, n_in, ld_in, nullptr, out, ld_out, rk, (hipStream_t)stream);
 }

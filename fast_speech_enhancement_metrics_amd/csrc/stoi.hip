@@ -635,6 +635,14 @@ inline int run(const float *ref, const float *deg, int64_t B, int64_t length, in
     const int64_t grid = nitems < (int64_t)ncu * 3 ? nitems : (int64_t)ncu * 3;  // 3 resident per CU
     hipLaunchKernelGGL(stoi_resample_vad16, dim3((unsigned)grid), dim3(256), 0, st, ref, deg, rows, ld, nchunk,
                        nitems, w.y10, g.y_ld, w.energy, g.nv_ld);
+  } else if (g.mode == 2) {
+    // other rates: tiled polyphase resampler into the 10 kHz rows, then the clean energies
+    rc = launch_resample_tiled(ref, B, length, ld, lengths, w.y10, 2 * g.y_ld, rk, st);
+    if (rc != FSEM_OK) return rc;
+    rc = launch_resample_tiled(deg, B, length, ld, lengths, w.y10 + g.y_ld, 2 * g.y_ld, rk, st);
+    if (rc != FSEM_OK) return rc;
+    hipLaunchKernelGGL(stoi_vad10, dim3((unsigned)std::max(1, (g.NV + VFE - 1) / VFE), (unsigned)B), dim3(256), 0,
+                       st, w.y10, g.y_ld, rows, w.energy, g.nv_ld);
   } else {
     hipLaunchKernelGGL(stoi_resample_vad, dim3((unsigned)((g.L10 + VF3 * 128 - 1) / (VF3 * 128)), (unsigned)B),
                        dim3(256), 0, st, ref, deg, rows, ld, g.mode, rk, w.y10, g.y_ld, w.energy, g.nv_ld);

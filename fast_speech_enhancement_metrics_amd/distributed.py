@@ -46,3 +46,57 @@ def sharded_scores(metric, clean: torch.Tensor, noisy: torch.Tensor, group=None,
     cols = res if isinstance(res, tuple) else (res,)
     local = torch.stack([c.to(torch.float32) for c in cols], dim=1)
     return gather_scores(local, B, group)
+
+
+def lpt_shards(lengths, world: int) -> list[list[int]]:
+    """Longest-processing-time assignment of ragged utterances to ranks:
+    utterances in decreasing length, each to the rank with the least total samples so far
+    (ties -> lowest rank).  Deterministic, so every rank computes the same plan locally."""
+    import heapq
+    order = sorted(range(len(lengths)), key=lambda i: (-int(lengths[i]), i))
+    heap = [(0, r) for r in range(world)]
+    shards: list[list[int]] = [[] for _ in range(world)]
+    for i in order:
+        load, r = heapq.heappop(heap)
+        shards[r].append(i)
+        heapq.heappush(heap, (load + int(lengths[i]), r))
+    return [sorted(s) for s in shards]
+
+
+def sharded_scores_ragged(metric, clean, noisy, group=None, device=None) -> torch.Tensor:
+    """Score a ragged batch (lists of 1-D utterances) data-parallel with LPT balancing by total
+    length: this rank scores its utterances as one padded batch with per-row lengths
+    (``metric.scores(..., lengths=...)``), then the [n_r, k] score rows are all-gathered and put
+    back in the caller's order -> [B, k] on every rank."""
+    from .batching import pad_batch
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    lengths = [int(x.numel()) for x in noisy]
+    plan = lpt_shards(lengths, world)
+    mine = plan[rank]
+    c, n, lens = pad_batch([clean[i] for i in mine], [noisy[i] for i in mine]) if mine else (None, None, None)
+    if device is not None and c is not None:
+        c, n = c.to(device), n.to(device)
+    if mine:
+        # STOI.scores takes the input rate (its resampler is fused); PESQ / PESQ_STOI take 16 kHz rows
+        kw = {"sample_rate": metric.sample_rate} if hasattr(metric, "N") else {}
+        res = metric.scores(c, n, lengths=lens, **kw)
+        cols = res if isinstance(res, tuple) else (res,)
+        local = torch.stack([x.to(torch.float32) for x in cols], dim=1)
+    else:
+        k = 3 if metric.__class__.__name__ == "PESQ_STOI" else (2 if hasattr(metric, "N") else 1)
+        local = torch.zeros(0, k, dtype=torch.float32, device=device or "cpu")
+    cap = max(len(s) for s in plan)
+    k = local.shape[1]
+    buf = torch.full((cap, k), float("nan"), dtype=torch.float32, device=local.device)
+    buf[:local.shape[0]] = local
+    out = torch.empty(world * cap, k, dtype=torch.float32, device=local.device)
+    if dist.get_backend(group) == "nccl":
+        dist.all_gather_into_tensor(out, buf, group=group)
+    else:
+        dist.all_gather(list(out.chunk(world)), buf, group=group)
+    full = torch.empty(len(lengths), k, dtype=torch.float32, device=local.device)
+    for r, idx in enumerate(plan):
+        if idx:
+            full[torch.tensor(idx, device=local.device)] = out[r * cap:r * cap + len(idx)]
+    return full

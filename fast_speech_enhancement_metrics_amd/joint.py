@@ -5,7 +5,9 @@ The reference computes the two metrics with two calls, each reading both signals
 (base.py:19-20 resampling to 10 kHz, STOI.py:153-205).  ``PESQ_STOI`` returns the same
 numbers -- on the GPU bitwise those of the two separate engine calls -- while the engine reads
 each input once: the PESQ front end's LDS tiles also feed the fused 16 -> 10 kHz resampler
-(``fsem_pesq_stoi_f32``).  Other input rates are resampled to 16 kHz first (BaseMetric).
+(``fsem_pesq_stoi_f32``).  At other input rates the two metrics keep the reference's own
+resampling paths (PESQ: sr -> 16 kHz, STOI: sr -> 10 kHz directly, base.py:19-20) and are
+computed by the PESQ and STOI engines separately.
 """
 from __future__ import annotations
 
@@ -25,11 +27,26 @@ class PESQ_STOI(BaseMetric):
 
     def __init__(self, sample_rate: int = 16000, use_gpu: bool = False):
         super().__init__(sample_rate, use_gpu)
-        self._pesq = PESQ(16000, use_gpu)
-        self._stoi = STOI(16000, use_gpu)
+        self._pesq = PESQ(sample_rate, use_gpu)
+        self._stoi = STOI(sample_rate, use_gpu)
+
+    def __call__(self, clean_speech, denoised_speech, lengths=None) -> list[dict[str, float]]:
+        if self.sample_rate == self.EXPECTED_SAMPLING_RATE:
+            return super().__call__(clean_speech, denoised_speech, lengths)
+        # STOI must resample sr -> 10 kHz itself (not via 16 kHz) to match the reference
+        p = self._pesq(clean_speech, denoised_speech, lengths)
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore", RuntimeWarning)
+            try:
+                s = self._stoi(clean_speech, denoised_speech, lengths)
+            except TypeError:  # no utterance has a STOI segment (STOI.py:162-165)
+                s = [{"STOI": float("nan"), "ESTOI": float("nan")}] * len(p)
+        return [{**a, **b} for a, b in zip(p, s)]
 
     def scores(self, clean_speech: torch.Tensor, denoised_speech: torch.Tensor, lengths=None):
         """(mos[B], stoi[B], estoi[B]) on the metric's device, 16 kHz rows (no host sync on GPU)."""
+        if self.sample_rate != self.EXPECTED_SAMPLING_RATE:
+            raise ValueError("PESQ_STOI.scores takes 16 kHz rows; call the metric for other rates")
         clean = as_rows(clean_speech)
         noisy = as_rows(denoised_speech)
         if noisy.shape != clean.shape:

@@ -61,3 +61,56 @@ def test_shard_bounds_cover_batch(batch, world):
     assert all(b[i][1] == b[i + 1][0] for i in range(world - 1))
     sizes = [hi - lo for lo, hi in b]
     assert max(sizes) - min(sizes) <= 1
+
+
+def _worker_ragged(rank, world, port, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from fast_speech_enhancement_metrics_amd import PESQ, STOI
+        from fast_speech_enhancement_metrics_amd.distributed import sharded_scores_ragged
+        from tests.conftest import load_golden
+        g = load_golden("varlen_16k")
+        cl = [torch.from_numpy(g["clean_f"][b, :n]) for b, n in enumerate(g["lengths"])]
+        dl = [torch.from_numpy(g["noisy_f"][b, :n]) for b, n in enumerate(g["lengths"])]
+        p = sharded_scores_ragged(PESQ(16000), cl, dl)
+        s = sharded_scores_ragged(STOI(16000), cl, dl)
+        out_q.put((rank, p.numpy(), s.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ragged_lpt_sharding_matches_reference():
+    """Config-5 style ragged batch over 2 gloo ranks (LPT by total length) == golden."""
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker_ragged, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    from tests.conftest import load_golden
+    g = load_golden("varlen_16k")
+    for rank, p, s in res:
+        for got, want, tol in ((p[:, 0], g["pesq"], 2e-3), (s[:, 0], g["stoi"], 1e-4), (s[:, 1], g["estoi"], 1e-4)):
+            assert np.array_equal(np.isnan(got), np.isnan(want))
+            m = ~np.isnan(want)
+            np.testing.assert_allclose(got[m], want[m], atol=tol, rtol=0)
+
+
+def test_lpt_shards_balance():
+    from fast_speech_enhancement_metrics_amd.distributed import lpt_shards
+    rng = np.random.default_rng(0)
+    lens = rng.integers(32000, 480000, size=1000)
+    plan = lpt_shards(lens, 8)
+    assert sorted(i for s in plan for i in s) == list(range(1000))
+    loads = [int(lens[s].sum()) for s in plan]
+    assert max(loads) - min(loads) <= lens.max()  # LPT bound
+    assert (max(loads) - min(loads)) / np.mean(loads) < 0.01

@@ -260,3 +260,26 @@ def test_gpu_front_y10_resampler_and_front_unchanged():
     assert np.isfinite(y[1::2, :L10]).all()
     assert lib.fsem_pesq_front_y10_f32(c.data_ptr(), d.data_ptr(), B, L, L, None, c.data_ptr(), c.data_ptr(),
                                        c.data_ptr(), L10 - 1, c.data_ptr(), 1 << 30, None) == -1
+
+
+def test_joint_8k_cpu_mode_matches_reference():
+    """PESQ_STOI(8000): PESQ via 8->16 kHz, STOI via 8->10 kHz directly, as the reference."""
+    from fast_speech_enhancement_metrics_amd import PESQ_STOI
+    g = load_golden("varlen_8k")
+    lens = g["lengths"]
+    cl = [torch.from_numpy(g["clean_f"][b, :n]) for b, n in enumerate(lens)]
+    dl = [torch.from_numpy(g["noisy_f"][b, :n]) for b, n in enumerate(lens)]
+    res = PESQ_STOI(8000)(cl, dl)
+    _close_with_nans([r["PESQ"] for r in res], g["pesq"], 2e-3)
+    _close_with_nans([r["STOI"] for r in res], g["stoi"], 1e-4)
+    _close_with_nans([r["ESTOI"] for r in res], g["estoi"], 1e-4)
+
+
+@pytest.mark.gpu
+def test_gpu_joint_8k_matches_reference():
+    from fast_speech_enhancement_metrics_amd import PESQ_STOI
+    g = load_golden("rate_8k")
+    res = PESQ_STOI(8000, use_gpu=True)(torch.from_numpy(g["clean_f"]), torch.from_numpy(g["noisy_f"]))
+    np.testing.assert_allclose([r["PESQ"] for r in res], g["pesq"], atol=PESQ_TOL, rtol=0)
+    np.testing.assert_allclose([r["STOI"] for r in res], g["stoi"], atol=STOI_TOL, rtol=0)
+    np.testing.assert_allclose([r["ESTOI"] for r in res], g["estoi"], atol=STOI_TOL, rtol=0)
