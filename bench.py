@@ -47,8 +47,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=5)
     ap.add_argument("--separate", action="store_true", help="two API calls (PESQ, STOI) instead of the joint entry")
-    ap.add_argument("--workload", default="c2", choices=["c2", "c5"],
-                    help="c2: BASELINE metric (default); c5: config 5, mixed 8/16 kHz ragged 2-30 s batch")
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c5"],
+                    help="c2: BASELINE metric (default); c3: STOI+ESTOI only, 8192 x 5 s @ 16 kHz per GPU; "
+                         "c5: config 5, mixed 8/16 kHz ragged 2-30 s batch")
     return ap.parse_args()
 
 
@@ -155,6 +156,58 @@ def pmc_traffic(kernel: str, B: int, L: int):
     return best if best else (None, None)
 
 
+def _timed(step, args, dev, distributed):
+    for _ in range(args.warmup):
+        step()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    if distributed:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    return dt
+
+
+def run_c3(args, world, rank, dev, distributed):
+    """BASELINE.json configs[2]: STOI+ESTOI of 8192 x 5 s @ 16 kHz pairs per GPU (fused 16->10 kHz)."""
+    from fast_speech_enhancement_metrics_amd import STOI
+    from fast_speech_enhancement_metrics_amd.synthetic import speech_like_pairs
+    B, L = 8192, 80000
+    cs, ns = [], []
+    for lo in range(0, B, 2048):
+        c, n, _ = speech_like_pairs(2048, L, 16000, seed=77 + 13 * rank + lo, device=dev)
+        cs.append(c)
+        ns.append(n)
+    clean, noisy = torch.cat(cs), torch.cat(ns)
+    del cs, ns
+    stoi = STOI(16000, use_gpu=True)
+
+    def step():
+        s, e = stoi.scores(clean, noisy, 16000)
+        local = torch.stack([s, e], 1)
+        return local.cpu() if rank == 0 else None
+
+    dt = _timed(step, args, dev, distributed)
+    if rank == 0:
+        print(json.dumps({
+            "metric": "utterances/sec STOI+ESTOI, 5s@16kHz, batch 8192 (config 3)",
+            "value": round(world * B * args.steps / dt, 2), "unit": "utterances/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic speech-like pairs",
+            "config": {"workload": "config 3: STOI/ESTOI scores, fused 16->10 kHz resampling",
+                       "batch_per_gpu": B, "length": L, "sample_rate": 16000,
+                       "parallelism": f"dp{world}"}}), flush=True)
+
+
 def run_c5(args, world, rank, dev, distributed):
     """BASELINE.json configs[4] / SURVEY 8(d) C5: 2048 utterances per GPU (16384 on 8), lengths
     uniform in 2-30 s, half at 8 kHz (PESQ via 8->16 kHz, STOI via 8->10 kHz, as the reference's
@@ -201,22 +254,7 @@ def run_c5(args, world, rank, dev, distributed):
         res = torch.cat([out8, out16])
         return res.cpu() if rank == 0 else None
 
-    for _ in range(args.warmup):
-        step()
-    if distributed:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    if distributed:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    dt = time.perf_counter() - t0
-    if distributed:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    dt = _timed(step, args, dev, distributed)
     if rank == 0:
         audio_s = float(secs.sum())
         print(json.dumps({
@@ -243,8 +281,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    if args.workload == "c5":
-        run_c5(args, world, rank, dev, distributed)
+    if args.workload in ("c3", "c5"):
+        (run_c3 if args.workload == "c3" else run_c5)(args, world, rank, dev, distributed)
         if distributed:
             dist.barrier()
             dist.destroy_process_group()
