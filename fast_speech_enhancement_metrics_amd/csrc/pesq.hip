@@ -63,12 +63,14 @@ constexpr int OWN = NF * 256;     // samples of band-pass power owned per segmen
 constexpr int NBARK = 49;
 constexpr int NS = 12;            // scan states: 10 band-pass (5 sections) + 2 pre-emphasis
 constexpr int SCAN_LD = 13;       // floats per lane in the scan buffer (odd: conflict-free)
-constexpr int XBUF = 4 * 2 * kFftBuf;  // 4 waves x 576 complex
+// exchange buffer: 4 waves x 576 complex for the FFTs, or the two halves of the double-buffered
+// chunk scan (2 x 256 x 13 floats); with the tile, 79 968 B per workgroup: 2 fit a CU
+constexpr int XBUF = 2 * PT * 13 > 4 * 2 * kFftBuf ? 2 * PT * 13 : 4 * 2 * kFftBuf;
 constexpr int SPEC_LD = 257;      // parked spectrum row stride (bank-conflict pad)
 constexpr int NBP = 10;           // band-pass states
 constexpr int PF = TILE / 4 / PT; // float4 per thread per tile (prefetch registers)
 static_assert(WARM + 256 * (NF + 1) == TILE, "tile geometry");
-static_assert(PT * SCAN_LD <= XBUF, "scan buffer fits the exchange buffer");
+static_assert(2 * PT * SCAN_LD <= XBUF, "double-buffered scan fits the exchange buffer");
 static_assert(SPEC_LD * (NF - 1) + 256 <= TILE, "parked spectra stay in the tile");
 static_assert(TILE % (4 * PT) == 0, "prefetch split");
 
@@ -322,7 +324,7 @@ __global__ void __launch_bounds__(PT, 2)
       rg.nseg = nseg;
     }
     if (VARLEN && it.g >= rg.nseg) {  // segment past this row's end: no samples, no frames
-      if (tid == 0) ppart[it.s * nseg + it.g] = 0.f;
+      if (tid < 4) ppart[(it.s * nseg + it.g) * 4 + tid] = 0.f;
       const int64_t nxt = item + gridDim.x;
       if (nxt < nitems) prefetch(make_item(nxt, nseg, B, ld, Lcap, lens, ref, deg), tid, pre);
       continue;
@@ -376,19 +378,20 @@ __global__ void __launch_bounds__(PT, 2)
       iir_pass1<false>(my4, t_lane, L, e);
     STAMP(2);
     // ---------------------------------------------------------------- chunk scan (4 levels)
-    float *const mine = xbuf + tid * SCAN_LD;
+    // double-buffered (read one half, write the other): one barrier per level
+    float *sbuf = xbuf;
+    float *dbuf = xbuf + PT * SCAN_LD;
 #pragma unroll
-    for (int i = 0; i < NS; ++i) mine[i] = e[i];
+    for (int i = 0; i < NS; ++i) sbuf[tid * SCAN_LD + i] = e[i];
     lds_barrier();
 #pragma unroll
     for (int lv = 0; lv < 4; ++lv) {
       const int d = 1 << lv;
       float q[NS];
-      const float *src = xbuf + max(tid - d, 0) * SCAN_LD;  // one base + immediate offsets
+      const float *src = sbuf + max(tid - d, 0) * SCAN_LD;  // one base + immediate offsets
       const float keep = (tid >= d) ? 1.f : 0.f;
 #pragma unroll
       for (int i = 0; i < NS; ++i) q[i] = src[i] * keep;
-      lds_barrier();
 #pragma unroll
       for (int i = 0; i < NBP; ++i) {
         float acc = e[i];
@@ -403,19 +406,17 @@ __global__ void __launch_bounds__(PT, 2)
         e[NBP] = p0;
         e[NBP + 1] = p1;
       }
-      if (lv < 3) {
 #pragma unroll
-        for (int i = 0; i < NS; ++i) mine[i] = e[i];
-        lds_barrier();
-      }
+      for (int i = 0; i < NS; ++i) dbuf[tid * SCAN_LD + i] = e[i];
+      lds_barrier();
+      float *t = sbuf;
+      sbuf = dbuf;
+      dbuf = t;
     }
     // start state of chunk j = inclusive prefix of chunk j-1
-#pragma unroll
-    for (int i = 0; i < NS; ++i) mine[i] = e[i];
-    lds_barrier();
     float z[NS];
     {
-      const float *src = xbuf + max(tid - 1, 0) * SCAN_LD;
+      const float *src = sbuf + max(tid - 1, 0) * SCAN_LD;
       const float keep = (tid >= 1) ? 1.f : 0.f;
 #pragma unroll
       for (int i = 0; i < NS; ++i) z[i] = src[i] * keep;
@@ -435,8 +436,9 @@ __global__ void __launch_bounds__(PT, 2)
         acc = iir_pass2<true, true>(w4, z, own_lo, own_hi, lim, t_lane, L);
       else
         acc = iir_pass2<false, true>(w4, z, own_lo, own_hi, lim, t_lane, L);
-      const float tot = block_sum_256(acc, red);
-      if (tid == 0) ppart[it.s * nseg + g] = tot * (kBpGain * kBpGain);
+      // per-wave partials (no workgroup barrier); pesq_power_sum adds them in a fixed order
+      const float tot = wave_sum(acc);
+      if (lane == 0) ppart[(it.s * nseg + g) * 4 + wave] = tot * (kBpGain * kBpGain);
     }
     lds_barrier();
     STAMP(4);
@@ -584,7 +586,7 @@ __global__ void __launch_bounds__(256) pesq_power_sum(const float *__restrict__ 
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nsig) return;
   float acc = 0.f;
-  for (int g = 0; g < nseg; ++g) acc += ppart[s * nseg + g];
+  for (int g = 0; g < 4 * nseg; ++g) acc += ppart[s * nseg * 4 + g];
   power[s] = acc;
 }
 
@@ -785,7 +787,7 @@ extern "C" int fsem_debug_read_stamps(void *dst, size_t bytes) {
 
 extern "C" size_t fsem_pesq_front_workspace_bytes(int64_t batch, int64_t length) {
   const pesq::Geometry g = pesq::geometry(length);
-  return align_up(sizeof(float) * (size_t)(2 * batch) * (size_t)g.nseg, 256);
+  return align_up(sizeof(float) * (size_t)(2 * batch) * (size_t)g.nseg * 4, 256);
 }
 
 extern "C" size_t fsem_pesq_workspace_bytes(int64_t batch, int64_t length) {
