@@ -599,10 +599,11 @@ __device__ __forceinline__ float pow_pos(float x, float e) {
 }
 
 __device__ __forceinline__ float loud(float p, int b) {
-  // loudness.py:64-65: (2T)^e ((0.5 + 0.5 P/T)^e - 1), 0 where P <= T; times Sl (folded)
+  // loudness.py:64-65: (2T)^e ((0.5 + 0.5 P/T)^e - 1), 0 where P <= T; times Sl (folded).
+  // 0.5 P/T as P * (0.5/T) (one rounding instead of a correctly rounded division: <=1 ulp)
   const float t = kThresh[b];
   if (!(p > t)) return 0.f;
-  return kLoud2TE[b] * (pow_pos(fmaf(0.5f, p / t, 0.5f), kLoudExp[b]) - 1.f);
+  return kLoud2TE[b] * (pow_pos(fmaf(p, kHalfInvThresh[b], 0.5f), kLoudExp[b]) - 1.f);
 }
 
 // Frames are processed in chunks of BC staged in LDS by coalesced loads ([frame][49] rows are
@@ -635,9 +636,8 @@ __global__ void __launch_bounds__(BT)
   }
   const float *__restrict__ bc = bark + (b * (int64_t)Fcap) * NBARK;
   const float *__restrict__ bn = bark + ((b + B) * (int64_t)Fcap) * NBARK;
-  float *__restrict__ silent = scratch + b * (int64_t)Fcap * 4;
-  float *__restrict__ afpc = silent + F;
-  float *__restrict__ sym = afpc + F;
+  // scratch row of this utterance: [sym | asym] per frame (stride 4 * Fcap, two slots unused)
+  float *__restrict__ sym = scratch + b * (int64_t)Fcap * 4;
   float *__restrict__ asym = sym + F;
   // PESQ.py:97-100 -- power = sum / (L + 5120) / 1.04684; bark scales by 1e7 / power
   const float pc = power[b] / (float)(L + 5120) / 1.04684f;
@@ -648,10 +648,10 @@ __global__ void __launch_bounds__(BT)
   float mc = 0.f, mn = 0.f;
   for (int f0 = 0; f0 < F; f0 += BC) {
     const int nf = min(BC, F - f0);
-    __syncthreads();
+    lds_barrier();  // LDS only: leaves the sym/asym stores in flight
     stage_chunk(C, bc + (int64_t)f0 * NBARK, nf, tid);
     stage_chunk(N, bn + (int64_t)f0 * NBARK, nf, tid);
-    __syncthreads();
+    lds_barrier();  // LDS only: leaves the sym/asym stores in flight
     if (tid < nf) {
       float a = 0.f;
 #pragma unroll 7
@@ -661,23 +661,23 @@ __global__ void __launch_bounds__(BT)
       }
       const float sil = (a < 1e7f) ? 1.f : 0.f;
       frs[tid] = sil;
-      silent[f0 + tid] = sil;
     }
-    __syncthreads();
+    lds_barrier();  // LDS only: leaves the sym/asym stores in flight
     if (lane < NBARK) {
       const float t100 = kThresh[lane] * 100.f;
+#pragma unroll 4
       for (int f = wave; f < nf; f += 2) {
-        if (frs[f] != 0.f) continue;
+        const float keep = (frs[f] == 0.f) ? 1.f : 0.f;  // silent frames excluded (branch-free)
         const float c = C[f * BLD + lane] * sc;
         const float n = N[f * BLD + lane] * sn;
-        mc += (c > t100) ? c : 0.f;
-        mn += (n > t100) ? n : 0.f;
+        mc += (c > t100) ? c * keep : 0.f;
+        mn += (n > t100) ? n * keep : 0.f;
       }
     }
   }
   bsum[wave][0][lane] = mc;
   bsum[wave][1][lane] = mn;
-  __syncthreads();
+  lds_barrier();  // LDS only: leaves the sym/asym stores in flight
   if (tid < NBARK) {
     const float c = (bsum[0][0][tid] + bsum[1][0][tid]) / F;
     const float n = (bsum[0][1][tid] + bsum[1][1][tid]) / F;
@@ -689,10 +689,10 @@ __global__ void __launch_bounds__(BT)
   float fr_prev = 0.f;  // frame power ratio of the last frame of the previous chunk
   for (int f0 = 0; f0 < F; f0 += BC) {
     const int nf = min(BC, F - f0);
-    __syncthreads();
+    lds_barrier();  // LDS only: leaves the sym/asym stores in flight
     stage_chunk(C, bc + (int64_t)f0 * NBARK, nf, tid);
     stage_chunk(N, bn + (int64_t)f0 * NBARK, nf, tid);
-    __syncthreads();
+    lds_barrier();  // LDS only: leaves the sym/asym stores in flight
     float ac = 0.f;
     if (tid < nf) {
       float an = 0.f;
@@ -706,14 +706,14 @@ __global__ void __launch_bounds__(BT)
       frs[tid + 1] = (ac + 5e3f) / (an + 5e3f);
     }
     if (tid == 0) frs[0] = fr_prev;
-    __syncthreads();
+    lds_barrier();  // LDS only: leaves the sym/asym stores in flight
     fr_prev = frs[nf];
     if (tid < nf) {
       const int f = f0 + tid;
       float r = (f >= 1) ? 0.8f * frs[tid + 1] + 0.2f * frs[tid] : frs[1];  // non-recursive (PESQ.py:161)
       r = fminf(fmaxf(r, 3e-4f), 5.f);
       float s2 = 0.f, as = 0.f;
-#pragma unroll 1
+#pragma unroll 7
       for (int k = 0; k < NBARK; ++k) {
         const float ec = ratio[k] * (C[tid * BLD + k] * sc);
         const float en = r * (N[tid * BLD + k] * sn);
@@ -724,7 +724,7 @@ __global__ void __launch_bounds__(BT)
         if (k >= 1) {
           const float wd = kWidthBark[k] * d;
           s2 = fmaf(wd, wd, s2);
-          float a = pow_pos((en + 50.f) / (ec + 50.f), 1.2f);
+          float a = pow_pos((en + 50.f) * __builtin_amdgcn_rcpf(ec + 50.f), 1.2f);  // ~1 ulp rcp
           a = (a < 3.f) ? 0.f : fminf(a, 12.f);
           as += fabsf(wd * a);
         }
@@ -736,7 +736,8 @@ __global__ void __launch_bounds__(BT)
       asym[f] = fminf(ay / w, 45.f);
     }
   }
-  __syncthreads();
+  lds_barrier();  // LDS only: leaves the sym/asym stores in flight
+  __syncthreads();  // full barrier: pass 3 reads other threads' sym / asym stores
   // ---- pass 3: L6 within 20-frame windows (hop 10), L2 across windows (PESQ.py:168-172)
   const int nw = (F - 20) / 10 + 1;
   double as_ = 0.0, aa_ = 0.0;
