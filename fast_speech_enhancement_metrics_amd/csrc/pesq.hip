@@ -66,7 +66,7 @@ constexpr int SCAN_LD = 13;       // floats per lane in the scan buffer (odd: co
 // exchange buffer: 4 waves x 576 complex for the FFTs, or the two halves of the double-buffered
 // chunk scan (2 x 256 x 13 floats); with the tile, 79 968 B per workgroup: 2 fit a CU
 constexpr int XBUF = 2 * PT * 13 > 4 * 2 * kFftBuf ? 2 * PT * 13 : 4 * 2 * kFftBuf;
-constexpr int SPEC_LD = 257;      // parked spectrum row stride (bank-conflict pad)
+constexpr int SPEC_LD = 258;      // parked spectrum row stride: = 2 mod 32, MFMA A reads conflict-free
 constexpr int NBP = 10;           // band-pass states
 constexpr int PF = TILE / 4 / PT; // float4 per thread per tile (prefetch registers)
 static_assert(WARM + 256 * (NF + 1) == TILE, "tile geometry");
