@@ -402,16 +402,16 @@ __global__ void __launch_bounds__(256)
 }
 
 // One lane per 30-frame segment m: x[j][t] = X[j][m + t], y likewise (STOI.py:121-198).
-// 128-lane workgroups; per-lane row statistics of the ESTOI time normalisation are parked
-// in LDS ([stat][band][lane], conflict-free) between the row pass and the column pass.
+// 128-lane workgroups, band envelopes staged in LDS (19 KB); the per-lane row statistics of
+// the ESTOI time normalisation stay in registers (uniform-index writes from the rolled band
+// loop), capped at 168 VGPRs: 3 waves per SIMD.
 constexpr int SEG_T = 128;
-__global__ void __launch_bounds__(SEG_T)
+__global__ void __launch_bounds__(SEG_T, 3)
     stoi_seg(const float *__restrict__ tob, int64_t B, int64_t tmax, const int *__restrict__ kept,
              float *__restrict__ stoi_out, float *__restrict__ estoi_out) {
   constexpr int W = SEG_T + NSEG;  // frames per pass
   constexpr int LDX = W + 1;
   __shared__ float X[NB][LDX], Y[NB][LDX];
-  __shared__ float stat[4][NB][SEG_T];  // mu_x, 1/|x - mu_x|, mu_y, 1/|y - mu_y|
   __shared__ double red[4];
   const int tid = threadIdx.x;
   const int64_t b = blockIdx.x;
@@ -440,6 +440,10 @@ __global__ void __launch_bounds__(SEG_T)
     const int m = m0 + tid;
     if (m < S) {
       float s_acc = 0.f;
+      // per-lane row statistics of the ESTOI time normalisation, kept in VGPRs: the band loop
+      // stays rolled and writes them with its uniform index (register-indexed moves)
+      float mux[NB], rx[NB], muy[NB], ry[NB];  // mu_x, 1/|x - mu_x|, mu_y, 1/|y - mu_y|
+#pragma unroll 1
       for (int j = 0; j < NB; ++j) {
         float x[NSEG], y[NSEG];
         float sx2 = 0.f, sy2 = 0.f, sx = 0.f, sy = 0.f;
@@ -475,20 +479,12 @@ __global__ void __launch_bounds__(SEG_T)
         const float ryn = dyy > 0.f ? __builtin_amdgcn_rsqf(dyy) : 0.f;
         const float rcn = dcc > 0.f ? __builtin_amdgcn_rsqf(dcc) : 0.f;
         s_acc = fmaf(dxc * rxn, rcn, s_acc);
-        stat[0][j][tid] = mx;
-        stat[1][j][tid] = rxn;
-        stat[2][j][tid] = my;
-        stat[3][j][tid] = ryn;
+        mux[j] = mx;
+        rx[j] = rxn;
+        muy[j] = my;
+        ry[j] = ryn;
       }
       // ESTOI: time-normalised rows, then band (column) normalisation (STOI.py:178-181)
-      float mux[NB], rx[NB], muy[NB], ry[NB];
-#pragma unroll
-      for (int j = 0; j < NB; ++j) {
-        mux[j] = stat[0][j][tid];
-        rx[j] = stat[1][j][tid];
-        muy[j] = stat[2][j][tid];
-        ry[j] = stat[3][j][tid];
-      }
       float e_acc = 0.f;
       for (int t = 0; t < NSEG; ++t) {
         float a[NB], c[NB];
