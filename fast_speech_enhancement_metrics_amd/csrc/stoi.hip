@@ -298,7 +298,8 @@ __global__ void __launch_bounds__(256)
              const int *__restrict__ kept, int nv_ld, float *__restrict__ tob, int64_t tmax) {
   __shared__ __attribute__((aligned(16))) float blk[2][TF + 1][128];
   __shared__ __attribute__((aligned(16))) float xbuf[4 * 2 * kFftBuf];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: kept indices by scalar loads
   const int64_t b = blockIdx.y;
   const int n = kept[b];
   const int T = n - 2;  // STFT frames of the overlap-added signal: 1 + ((n+1)*128 - 512)/128
@@ -309,34 +310,33 @@ __global__ void __launch_bounds__(256)
   const int *kidx = idx + b * nv_ld;
   const float *__restrict__ yc = y10 + (b * 2) * y_ld;
   const float *__restrict__ yd = yc + y_ld;
-  auto at = [L10](const float *__restrict__ y, int64_t o) { return (o < L10) ? y[o] : 0.f; };
+  // range-checked raw buffer loads over each row's [0, L10): samples past the row end read as 0
+  // without a branch per load (torchaudio's zero padding of the overlap-added signal)
+  auto row_rsrc = [L10](const float *y) {
+    const uint64_t base = reinterpret_cast<uint64_t>(y);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
+    void *p = reinterpret_cast<void *>(((uint64_t)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(p, 0, __builtin_amdgcn_readfirstlane((uint32_t)(L10 * 4)), 0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t rc = row_rsrc(yc), rd = row_rsrc(yd);
+  auto at = [](__amdgpu_buffer_rsrc_t r, int64_t o) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)(o * 4), 0, 0));
+  };
   const float w_lo = kHann256s[lane], w_lo2 = kHann256s[lane + 64];
   const float w_hi = kHann256s[128 + lane], w_hi2 = kHann256s[128 + 64 + lane];
 
   // overlap-added blocks q = k0+1 .. kend+1:  block_q[t] = w[t] F_{i_q}[t] + w[128+t] F_{i_{q-1}}[128+t]
   const int nblk = kend - k0 + 1;
+#pragma unroll 3  // three blocks' loads in flight per wave
   for (int j = wave; j < nblk; j += 4) {
     const int q = k0 + 1 + j;
     const int iq = kidx[q], ip = kidx[q - 1];
     const int64_t a0 = 128LL * iq, a1 = 128LL * ip + 128;
-    float c0, c1, d0, d1;
-    if (a0 == a1) {  // consecutive kept frames: the two halves are the same samples
-      const float xc0 = at(yc, a0 + lane);
-      const float xc1 = at(yc, a0 + 64 + lane);
-      const float xd0 = at(yd, a0 + lane);
-      const float xd1 = at(yd, a0 + 64 + lane);
-      c0 = w_lo * xc0 + w_hi * xc0;
-      c1 = w_lo2 * xc1 + w_hi2 * xc1;
-      d0 = w_lo * xd0 + w_hi * xd0;
-      d1 = w_lo2 * xd1 + w_hi2 * xd1;
-    } else {
-      c0 = w_lo * at(yc, a0 + lane) + w_hi * at(yc, a1 + lane);
-      c1 = w_lo2 * at(yc, a0 + 64 + lane) +
-           w_hi2 * at(yc, a1 + 64 + lane);
-      d0 = w_lo * at(yd, a0 + lane) + w_hi * at(yd, a1 + lane);
-      d1 = w_lo2 * at(yd, a0 + 64 + lane) +
-           w_hi2 * at(yd, a1 + 64 + lane);
-    }
+    const float c0 = w_lo * at(rc, a0 + lane) + w_hi * at(rc, a1 + lane);
+    const float c1 = w_lo2 * at(rc, a0 + 64 + lane) + w_hi2 * at(rc, a1 + 64 + lane);
+    const float d0 = w_lo * at(rd, a0 + lane) + w_hi * at(rd, a1 + lane);
+    const float d1 = w_lo2 * at(rd, a0 + 64 + lane) + w_hi2 * at(rd, a1 + 64 + lane);
     blk[0][j][lane] = c0;
     blk[0][j][lane + 64] = c1;
     blk[1][j][lane] = d0;
