@@ -286,7 +286,8 @@ __global__ void __launch_bounds__(PT, 2)
   __shared__ __attribute__((aligned(16))) float xbuf[XBUF];
   __shared__ float red[8];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar branches)
   const int32_t *__restrict__ lens = VARLEN ? lens_arg : nullptr;  // uniform batches: no per-row lookups
   if (JOINT && tid < TILE_PAD) tile[TILE + tid] = 0.f;  // never rewritten
   // ---- per-lane constants, loaded once
@@ -626,7 +627,8 @@ __global__ void __launch_bounds__(BT)
   __shared__ float frs[BC + 1];
   __shared__ double dred[4];
   __shared__ float bsum[2][2][64];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar branches)
   const int64_t b = blockIdx.x;
   const int64_t L = row_length(lens, b, Lcap);
   const int F = frames_of(L);  // this utterance's frames; rows are laid out with stride Fcap

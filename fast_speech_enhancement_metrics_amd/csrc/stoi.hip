@@ -82,7 +82,8 @@ __global__ void __launch_bounds__(256, 2)
                         float *__restrict__ energy, int nv_ld) {
   __shared__ __attribute__((aligned(16))) float xin[XPF * 256 * 4 + 4];
   __shared__ __attribute__((aligned(16))) float ytile[YT + 8];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar branches)
   auto item_src = [&](int64_t item, int64_t &b, int &chunk, int &sig, int64_t &o0, int64_t &i0) {
     sig = (int)(item & 1);
     const int64_t bc = item >> 1;
@@ -203,7 +204,8 @@ __global__ void __launch_bounds__(256)
                       int mode, ResampleKernel rk, float *__restrict__ y10, int64_t y_ld,
                       float *__restrict__ energy, int nv_ld) {
   __shared__ __attribute__((aligned(16))) float ytile[YT3];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar branches)
   const int64_t b = blockIdx.y;
   const int64_t o0 = (int64_t)blockIdx.x * (VF3 * 128);
   const int64_t n_in = rows.n(b), L10 = rows.l10(b);
@@ -242,7 +244,8 @@ __global__ void __launch_bounds__(256)
 constexpr int VFE = 64;  // VAD frames per workgroup
 __global__ void __launch_bounds__(256)
     stoi_vad10(const float *__restrict__ y10, int64_t y_ld, Rows rows, float *__restrict__ energy, int nv_ld) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar branches)
   const int64_t b = blockIdx.y;
   const int NV = rows.nv(b);
   const float *__restrict__ yc = y10 + (2 * b) * y_ld;
@@ -268,7 +271,8 @@ __global__ void __launch_bounds__(256)
                 int *__restrict__ kept) {
   __shared__ float red[8];
   __shared__ int wcount[4];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar branches)
   const int64_t b = blockIdx.x;
   const int NV = rows.nv(b);
   const float *e = energy + b * nv_ld;
