@@ -37,10 +37,13 @@ __device__ __forceinline__ void dft8(cf v[8]) {
   v[7] = csub(b3, w3c3);
 }
 
-// LDS exchange area per wave, in float2: 512 + 64 pad (index i stored at i + i/8, which
-// makes the stage-0/1 scatters and the strided gathers bank-conflict-free).
-constexpr int kFftBuf = 576;
-__device__ __forceinline__ int fpad(int i) { return i + (i >> 3); }
+// LDS exchange area per wave: 512 float2, element i stored at fsw(i) = i ^ ((i >> 3) & 15).
+// The XOR swizzle keeps all four access patterns bank-conflict-free under the gfx950 LDS
+// lane-group rules (stage scatters 8*lane + r and o1 + 8r as ds_write_b64 in 16-lane groups,
+// gathers lane + 64r as ds_read_b64 in 32-lane groups) without padding; the former i + i/8
+// padding left 2-way conflicts on the gathers.
+constexpr int kFftBuf = 512;
+__device__ __forceinline__ int fpad(int i) { return i ^ ((i >> 3) & 15); }
 
 // 512-point complex FFT of one wave, radix-8 Stockham, natural-order result in
 // v[r] = Z[lane + 64 r].  `buf` = this wave's kFftBuf-float2 LDS exchange area.
