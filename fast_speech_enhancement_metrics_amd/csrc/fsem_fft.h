@@ -45,36 +45,78 @@ __device__ __forceinline__ void dft8(cf v[8]) {
 constexpr int kFftBuf = 512;
 __device__ __forceinline__ int fpad(int i) { return i ^ ((i >> 3) & 15); }
 
+// Packed-FP32 form of the butterflies: complex values as float2 vectors, so additions become
+// v_pk_add_f32 and the multiplications by -i, (1-i)/sqrt2, (-1-i)/sqrt2 fold into v_pk_fma_f32
+// with swapped operands (op_sel) -- on gfx950 one packed instruction costs the issue slot of
+// one scalar one (tools/micro/valu_rate.hip: 2x the FP32 rate).  IEEE per element, so the
+// arithmetic per element is that of the scalar form up to the fused multiply-adds.
+typedef float f2 __attribute__((ext_vector_type(2)));
+#define FSEM_FMA2 __builtin_elementwise_fma
+
+__device__ __forceinline__ f2 cmul2(f2 a, f2 b) {  // a * b
+  const f2 t = a.xx * b;
+  return FSEM_FMA2(b.yx, (f2){-a.y, a.y}, t);
+}
+
+__device__ __forceinline__ void dft8v(f2 v[8]) {
+  const f2 pm = {1.f, -1.f}, mp = {-1.f, 1.f};
+  const float h = 0.70710678118654752f;
+  const f2 hh = {h, h}, nh = {-h, -h};
+  const f2 a0 = v[0] + v[4], a1 = v[0] - v[4];
+  const f2 a2 = v[2] + v[6], d26 = v[2] - v[6];
+  const f2 a4 = v[1] + v[5], a5 = v[1] - v[5];
+  const f2 a6 = v[3] + v[7], d37 = v[3] - v[7];
+  const f2 b0 = a0 + a2, b2 = a0 - a2;
+  const f2 b1 = FSEM_FMA2(d26.yx, pm, a1), b3 = FSEM_FMA2(d26.yx, mp, a1);  // a1 -/+ i d26
+  const f2 c0 = a4 + a6, c2 = a4 - a6;
+  const f2 c1 = FSEM_FMA2(d37.yx, pm, a5), c3 = FSEM_FMA2(d37.yx, mp, a5);
+  const f2 t1 = FSEM_FMA2(c1.yx, pm, c1);   // c1 (1 - i)
+  const f2 t3 = FSEM_FMA2(c3.yx, pm, -c3);  // c3 (-1 - i)
+  v[0] = b0 + c0;
+  v[4] = b0 - c0;
+  v[1] = FSEM_FMA2(t1, hh, b1);
+  v[5] = FSEM_FMA2(t1, nh, b1);
+  v[2] = FSEM_FMA2(c2.yx, pm, b2);  // b2 - i c2
+  v[6] = FSEM_FMA2(c2.yx, mp, b2);
+  v[3] = FSEM_FMA2(t3, hh, b3);
+  v[7] = FSEM_FMA2(t3, nh, b3);
+}
+
 // 512-point complex FFT of one wave, radix-8 Stockham, natural-order result in
 // v[r] = Z[lane + 64 r].  `buf` = this wave's kFftBuf-float2 LDS exchange area.
-__device__ __forceinline__ void fft512_wave(cf v[8], float2 *buf, int lane, const cf tw1[8],
+__device__ __forceinline__ void fft512_wave(cf vc[8], float2 *buf, int lane, const cf tw1[8],
                                             const cf tw2[8]) {
-  dft8(v);
+  f2 v[8];
 #pragma unroll
-  for (int r = 0; r < 8; ++r) buf[fpad(8 * lane + r)] = make_float2(v[r].r, v[r].i);
+  for (int r = 0; r < 8; ++r) v[r] = (f2){vc[r].r, vc[r].i};
+  dft8v(v);
+#pragma unroll
+  for (int r = 0; r < 8; ++r) buf[fpad(8 * lane + r)] = make_float2(v[r].x, v[r].y);
   wave_lds_fence();
 #pragma unroll
   for (int r = 0; r < 8; ++r) {
     float2 t = buf[fpad(lane + 64 * r)];
-    v[r] = {t.x, t.y};
+    v[r] = (f2){t.x, t.y};
   }
 #pragma unroll
-  for (int r = 1; r < 8; ++r) v[r] = cmul(v[r], tw1[r]);
-  dft8(v);
+  for (int r = 1; r < 8; ++r) v[r] = cmul2(v[r], (f2){tw1[r].r, tw1[r].i});
+  dft8v(v);
   wave_lds_fence();
   const int o1 = (lane >> 3) * 64 + (lane & 7);
 #pragma unroll
-  for (int r = 0; r < 8; ++r) buf[fpad(o1 + 8 * r)] = make_float2(v[r].r, v[r].i);
+  for (int r = 0; r < 8; ++r) buf[fpad(o1 + 8 * r)] = make_float2(v[r].x, v[r].y);
   wave_lds_fence();
 #pragma unroll
   for (int r = 0; r < 8; ++r) {
     float2 t = buf[fpad(lane + 64 * r)];
-    v[r] = {t.x, t.y};
+    v[r] = (f2){t.x, t.y};
   }
 #pragma unroll
-  for (int r = 1; r < 8; ++r) v[r] = cmul(v[r], tw2[r]);
-  dft8(v);
+  for (int r = 1; r < 8; ++r) v[r] = cmul2(v[r], (f2){tw2[r].r, tw2[r].i});
+  dft8v(v);
   wave_lds_fence();
+#pragma unroll
+  for (int r = 0; r < 8; ++r) vc[r] = {v[r].x, v[r].y};
 }
 
 
