@@ -4,14 +4,21 @@
 #include "fsem_common.h"
 
 namespace fsem {
+// A side stream on `st`'s device (one per device, created on first use, lives with the process)
+// for work that can overlap the caller's stream; `st` itself when none can be had.
+hipStream_t side_stream(hipStream_t st);
+// Make `waiter` wait for everything queued on `producer` so far (no-op when they are the same).
+int stream_wait(hipStream_t waiter, hipStream_t producer);
+
 namespace pesq {
 // pesq_front + power sums; with y10 != nullptr also writes the rows' 10 kHz resampled signals
 // ([2*batch, y_ld], row 2b = clean b, 2b+1 = denoised b) from the same LDS tiles.
 int launch_front(const float *ref, const float *deg, int64_t batch, int64_t length, int64_t ld,
                  const int32_t *lengths, float *bark, float *power, void *ws, size_t ws_bytes, float *y10,
                  int64_t y_ld, hipStream_t st);
-// whole PESQ-wb (front + back), optionally emitting y10 as above
+// whole PESQ-wb (front + back), optionally emitting y10 as above; the back end runs on back_st
+// after the front end on st (back_st == st: one stream)
 int run_wb(const float *ref, const float *deg, int64_t batch, int64_t length, int64_t ld, const int32_t *lengths,
-           float *mos, void *ws, size_t ws_bytes, float *y10, int64_t y_ld, hipStream_t st);
+           float *mos, void *ws, size_t ws_bytes, float *y10, int64_t y_ld, hipStream_t st, hipStream_t back_st);
 }  // namespace pesq
 }  // namespace fsem

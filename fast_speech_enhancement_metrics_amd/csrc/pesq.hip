@@ -32,6 +32,7 @@
 //   frame equalisation, Zwicker loudness, symmetric / asymmetric disturbance, L6/L2 pooling
 //   and the MOS mapping (PESQ.py:142-245), deterministic block reductions.
 #include <algorithm>
+#include <mutex>
 
 #include "fsem_fft.h"
 #include "fsem_internal.h"
@@ -866,9 +867,35 @@ extern "C" int fsem_pesq_back_f32(const float *bark, const float *power, int64_t
   return FSEM_OK;
 }
 
+hipStream_t fsem::side_stream(hipStream_t st) {
+  constexpr int kMaxDev = 64;
+  static std::mutex mu;
+  static hipStream_t side[kMaxDev] = {};
+  int cur = 0;
+  hipDevice_t dev = 0;
+  if (hipGetDevice(&cur) != hipSuccess || hipStreamGetDevice(st, &dev) != hipSuccess) return st;
+  // created on the current device only; a stream of another device keeps its work on one stream
+  if (dev != cur || dev < 0 || dev >= kMaxDev) return st;
+  std::lock_guard<std::mutex> lock(mu);
+  if (!side[dev] && hipStreamCreateWithFlags(&side[dev], hipStreamNonBlocking) != hipSuccess) {
+    side[dev] = nullptr;
+    return st;
+  }
+  return side[dev];
+}
+
+int fsem::stream_wait(hipStream_t waiter, hipStream_t producer) {
+  if (waiter == producer) return FSEM_OK;
+  hipEvent_t ev;  // one event per edge: concurrent callers never share a record
+  if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return FSEM_ELAUNCH;
+  const bool ok = hipEventRecord(ev, producer) == hipSuccess && hipStreamWaitEvent(waiter, ev, 0) == hipSuccess;
+  (void)hipEventDestroy(ev);  // released once the recorded work completes
+  return ok ? FSEM_OK : FSEM_ELAUNCH;
+}
+
 int fsem::pesq::run_wb(const float *ref, const float *deg, int64_t batch, int64_t length, int64_t ld,
                        const int32_t *lengths, float *mos, void *ws, size_t ws_bytes, float *y10, int64_t y_ld,
-                       hipStream_t stream) {
+                       hipStream_t stream, hipStream_t back_st) {
   if (!ref || !deg || !mos || batch <= 0 || length <= 0 || ld < length) return FSEM_EINVAL;
   const pesq::Geometry g = pesq::geometry(length);
   if (g.F < 20 && !lengths) return FSEM_ESHORT;
@@ -881,12 +908,15 @@ int fsem::pesq::run_wb(const float *ref, const float *deg, int64_t batch, int64_
   p += align_up(sizeof(float) * (size_t)(2 * batch), 256);
   int rc = pesq::launch_front(ref, deg, batch, length, ld, lengths, bark, power, ws, front, y10, y_ld, stream);
   if (rc != FSEM_OK) return rc;
+  rc = stream_wait(back_st, stream);
+  if (rc != FSEM_OK) return rc;
   return fsem_pesq_back_f32(bark, power, batch, length, lengths, mos, p,
-                            fsem_pesq_back_workspace_bytes(batch, length), stream);
+                            fsem_pesq_back_workspace_bytes(batch, length), back_st);
 }
 
 extern "C" int fsem_pesq_wb_f32(const float *ref, const float *deg, int64_t batch, int64_t length,
                                 int64_t ld, const int32_t *lengths, float *mos, void *ws, size_t ws_bytes,
                                 void *stream) {
-  return pesq::run_wb(ref, deg, batch, length, ld, lengths, mos, ws, ws_bytes, nullptr, 0, (hipStream_t)stream);
+  return pesq::run_wb(ref, deg, batch, length, ld, lengths, mos, ws, ws_bytes, nullptr, 0, (hipStream_t)stream,
+                       (hipStream_t)stream);
 }

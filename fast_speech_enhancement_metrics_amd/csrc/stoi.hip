@@ -704,13 +704,18 @@ extern "C" int fsem_pesq_stoi_f32(const float *ref, const float *deg, int64_t ba
   stoi::Ws w = stoi::carve(static_cast<char *>(ws) + pesq_bytes, batch, g);
   const stoi::Rows rows{lengths, length, rk.orig, rk.nw};
   hipStream_t st = (hipStream_t)stream;
-  // PESQ-wb with the 10 kHz rows emitted from the same input tiles
-  rc = pesq::run_wb(ref, deg, batch, length, ld, lengths, mos, ws, pesq_bytes, w.y10, g.y_ld, st);
+  // PESQ-wb with the 10 kHz rows emitted from the same input tiles.  The PESQ back end (one
+  // workgroup per pair, low occupancy) runs on a side stream concurrently with the STOI tail;
+  // both only read what the front end wrote, and the caller's stream joins the side stream.
+  const hipStream_t side = side_stream(st);
+  rc = pesq::run_wb(ref, deg, batch, length, ld, lengths, mos, ws, pesq_bytes, w.y10, g.y_ld, st, side);
   if (rc != FSEM_OK) return rc;
   hipLaunchKernelGGL(stoi::stoi_vad10, dim3((unsigned)std::max(1, (g.NV + stoi::VFE - 1) / stoi::VFE), (unsigned)batch),
                      dim3(256), 0, st, w.y10, g.y_ld, rows, w.energy, g.nv_ld);
   FSEM_CHECK_LAUNCH();
-  return stoi::run_tail(batch, g, rows, w.y10, w.energy, w.idx, w.kept, w.tob, g.tmax, stoi_out, estoi_out, st);
+  rc = stoi::run_tail(batch, g, rows, w.y10, w.energy, w.idx, w.kept, w.tob, g.tmax, stoi_out, estoi_out, st);
+  const int rj = stream_wait(st, side);
+  return rc != FSEM_OK ? rc : rj;
 }
 
 extern "C" const char *fsem_strerror(int code) {
