@@ -238,6 +238,14 @@ __device__ __forceinline__ void resample_tile(const float *__restrict__ tile, in
                                               float *__restrict__ yrow, float *__restrict__ stage, int lane,
                                               int wave) {
   const int ngrp = (int)((o_hi - o_lo + 4) / 5);
+  // opaque staging indices 5*lane + jj: adjacent stores would seed the SLP vectorizer, which
+  // pairs the five FMA chains into packed FMAs with SGPR coefficient pairs (SGPR spills)
+  int sidx[5];
+#pragma unroll
+  for (int jj = 0; jj < 5; ++jj) {
+    sidx[jj] = 5 * lane + jj;
+    asm volatile("" : "+v"(sidx[jj]));
+  }
   for (int j0 = 64 * wave; j0 < ngrp; j0 += 64 * (PT / 64)) {
     const int j = j0 + lane;
     if (j < ngrp) {
@@ -256,20 +264,19 @@ __device__ __forceinline__ void resample_tile(const float *__restrict__ tile, in
         float acc = 0.f;
 #pragma unroll
         for (int t = 0; t < 28; ++t) acc = fmaf(kRs16k10k[jj][t], v[t + 2], acc);
-        // phase-major staging (output 5*lane + jj at jj*64 + lane): conflict-free, and no
-        // adjacent stores for the SLP vectorizer to pair into SGPR-literal packed FMAs
-        stage[64 * jj + lane] = acc;
+        // output-major staging: stride-5 dword writes are conflict-free (gcd(5, 64) = 1)
+        stage[sidx[jj]] = acc;
       }
     }
     wave_lds_fence();
     const int64_t ob = o_lo + 5 * (int64_t)j0;  // multiple of 4: aligned float4 stores
     const int n = (int)min((int64_t)RS_STAGE, o_hi - ob);
-    auto at = [&](int c) { return stage[64 * (c % 5) + c / 5]; };
+    const float4 *__restrict__ s4 = reinterpret_cast<const float4 *>(stage);
     for (int q = lane; 4 * q < n; q += 64) {
       if (4 * q + 3 < n) {
-        reinterpret_cast<float4 *>(yrow + ob)[q] = make_float4(at(4 * q), at(4 * q + 1), at(4 * q + 2), at(4 * q + 3));
+        reinterpret_cast<float4 *>(yrow + ob)[q] = s4[q];
       } else {
-        for (int c = 4 * q; c < n; ++c) yrow[ob + c] = at(c);
+        for (int c = 4 * q; c < n; ++c) yrow[ob + c] = stage[c];
       }
     }
     wave_lds_fence();
