@@ -227,49 +227,55 @@ __device__ __forceinline__ float iir_pass2(float4 *__restrict__ w4, float z[NS],
 constexpr int OWN10 = OWN / 8 * 5;  // 7680
 constexpr int TILE_PAD = 16;        // zeros after the tile: the last segment's final taps
 static_assert(OWN % 8 == 0, "segments start on polyphase-group boundaries");
-static_assert(4 * 320 <= XBUF, "resampler staging fits the exchange buffer");
 static_assert((WARM - 12) % 4 == 0, "16-byte aligned tap reads");
 static_assert(WARM - 12 + 8 * ((TILE - WARM) * 5 / 8 / 5 - 1) + 32 <= TILE + TILE_PAD, "tap reads stay in the pad");
 
-// One wave resamples 64 consecutive groups (320 outputs) per step; the outputs are staged in
-// the wave's slice of the (then idle) exchange buffer and leave as aligned float4 stores.
-constexpr int RS_STAGE = 320;
+// Each lane resamples RS_RUN consecutive groups from one sliding window of taps (8 new inputs
+// per further group), so a wave step covers 64 * RS_RUN groups: 16 tap reads per group instead
+// of 28, and lane windows 96 B apart (two-way b128 bank pattern).  Outputs are staged in the
+// wave's slice of the (then idle) exchange buffer and leave as aligned float4 stores.
+constexpr int RS_RUN = 3;
+constexpr int RS_STAGE = 64 * RS_RUN * 5;  // outputs per wave step
+static_assert(4 * RS_STAGE <= XBUF, "resampler staging fits the exchange buffer");
 __device__ __forceinline__ void resample_tile(const float *__restrict__ tile, int64_t o_lo, int64_t o_hi,
                                               float *__restrict__ yrow, float *__restrict__ stage, int lane,
                                               int wave) {
   const int ngrp = (int)((o_hi - o_lo + 4) / 5);
-  // opaque staging indices 5*lane + jj: adjacent stores would seed the SLP vectorizer, which
-  // pairs the five FMA chains into packed FMAs with SGPR coefficient pairs (SGPR spills)
+  // opaque staging indices RS_RUN*5*lane + jj: adjacent stores would seed the SLP vectorizer,
+  // which pairs the five FMA chains into packed FMAs with SGPR coefficient pairs (SGPR spills)
   int sidx[5];
 #pragma unroll
   for (int jj = 0; jj < 5; ++jj) {
-    sidx[jj] = 5 * lane + jj;
+    sidx[jj] = RS_RUN * 5 * lane + jj;
     asm volatile("" : "+v"(sidx[jj]));
   }
-  for (int j0 = 64 * wave; j0 < ngrp; j0 += 64 * (PT / 64)) {
-    const int j = j0 + lane;
-    if (j < ngrp) {
-      const float4 *x4 = reinterpret_cast<const float4 *>(tile + (WARM - 12) + 8 * j);
-      float v[32];
+  for (int st = 0;; ++st) {
+    const int g0 = 64 * RS_RUN * (4 * st + wave);  // first group of this wave step (uniform)
+    if (g0 >= ngrp) break;
+    // groups past ngrp read whatever follows (in the LDS allocation) and are never stored
+    const float4 *x4 = reinterpret_cast<const float4 *>(tile + (WARM - 12) + 8 * (g0 + RS_RUN * lane));
+    float v[8 * RS_RUN + 24];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const float4 f = x4[q];
-        v[4 * q] = f.x;
-        v[4 * q + 1] = f.y;
-        v[4 * q + 2] = f.z;
-        v[4 * q + 3] = f.w;
-      }
+    for (int q = 0; q < 2 * RS_RUN + 6; ++q) {
+      const float4 f = x4[q];
+      v[4 * q] = f.x;
+      v[4 * q + 1] = f.y;
+      v[4 * q + 2] = f.z;
+      v[4 * q + 3] = f.w;
+    }
+#pragma unroll
+    for (int k = 0; k < RS_RUN; ++k) {
 #pragma unroll
       for (int jj = 0; jj < 5; ++jj) {
         float acc = 0.f;
 #pragma unroll
-        for (int t = 0; t < 28; ++t) acc = fmaf(kRs16k10k[jj][t], v[t + 2], acc);
-        // output-major staging: stride-5 dword writes are conflict-free (gcd(5, 64) = 1)
-        stage[sidx[jj]] = acc;
+        for (int t = 0; t < 28; ++t) acc = fmaf(kRs16k10k[jj][t], v[8 * k + t + 2], acc);
+        // output-major staging: stride-15 dword writes are conflict-free (gcd(15, 64) = 1)
+        stage[sidx[jj] + 5 * k] = acc;
       }
     }
     wave_lds_fence();
-    const int64_t ob = o_lo + 5 * (int64_t)j0;  // multiple of 4: aligned float4 stores
+    const int64_t ob = o_lo + 5 * (int64_t)g0;  // multiple of 4: aligned float4 stores
     const int n = (int)min((int64_t)RS_STAGE, o_hi - ob);
     const float4 *__restrict__ s4 = reinterpret_cast<const float4 *>(stage);
     for (int q = lane; 4 * q < n; q += 64) {
