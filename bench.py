@@ -103,11 +103,14 @@ def kernel_roofline(clean, noisy, reps, joint):
     h = stream.cuda_stream
     y_ld = ((5 * L + 7) // 8 + 63) // 64 * 64
     y10 = torch.empty(2 * B, y_ld, device=dev) if joint else None
+    v_ld = (((5 * L + 7) // 8) // 64 + 1 + 63) // 64 * 64
+    vad = torch.empty(B, v_ld, 2, device=dev) if joint else None  # STOI VAD quarter sums, as in the joint path
 
     def launch():
         if joint:
             rc = lib.fsem_pesq_front_y10_f32(clean.data_ptr(), noisy.data_ptr(), B, L, L, None, bark.data_ptr(),
-                                             power.data_ptr(), y10.data_ptr(), y_ld, ws.data_ptr(), ws.numel(), h)
+                                             power.data_ptr(), y10.data_ptr(), y_ld, vad.data_ptr(), v_ld,
+                                             ws.data_ptr(), ws.numel(), h)
         else:
             rc = lib.fsem_pesq_front_f32(clean.data_ptr(), noisy.data_ptr(), B, L, L, None, bark.data_ptr(),
                                          power.data_ptr(), ws.data_ptr(), ws.numel(), h)

@@ -43,7 +43,7 @@ SIGNATURES = {
     "fsem_pesq_front_workspace_bytes": (_c_sz, [_c_i64, _c_i64]),
     "fsem_pesq_front_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _c_sz, _vp]),
     "fsem_pesq_front_y10_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _c_i64,
-                                                _vp, _c_sz, _vp]),
+                                                _vp, _c_i64, _vp, _c_sz, _vp]),
     "fsem_pesq_back_workspace_bytes": (_c_sz, [_c_i64, _c_i64]),
     "fsem_pesq_back_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _vp, _vp, _vp, _c_sz, _vp]),
     "fsem_stoi_workspace_bytes": (_c_sz, [_c_i64, _c_i64, _c_i32]),

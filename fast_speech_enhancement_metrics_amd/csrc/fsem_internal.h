@@ -12,13 +12,15 @@ int stream_wait(hipStream_t waiter, hipStream_t producer);
 
 namespace pesq {
 // pesq_front + power sums; with y10 != nullptr also writes the rows' 10 kHz resampled signals
-// ([2*batch, y_ld], row 2b = clean b, 2b+1 = denoised b) from the same LDS tiles.
+// ([2*batch, y_ld], row 2b = clean b, 2b+1 = denoised b) from the same LDS tiles, and with
+// vad != nullptr the clean rows' STOI VAD quarter sums ([batch, v_ld] float2, fsem_vad.h).
 int launch_front(const float *ref, const float *deg, int64_t batch, int64_t length, int64_t ld,
                  const int32_t *lengths, float *bark, float *power, void *ws, size_t ws_bytes, float *y10,
-                 int64_t y_ld, hipStream_t st);
+                 int64_t y_ld, float2 *vad, int64_t v_ld, hipStream_t st);
 // whole PESQ-wb (front + back), optionally emitting y10 as above; the back end runs on back_st
 // after the front end on st (back_st == st: one stream)
 int run_wb(const float *ref, const float *deg, int64_t batch, int64_t length, int64_t ld, const int32_t *lengths,
-           float *mos, void *ws, size_t ws_bytes, float *y10, int64_t y_ld, hipStream_t st, hipStream_t back_st);
+           float *mos, void *ws, size_t ws_bytes, float *y10, int64_t y_ld, float2 *vad, int64_t v_ld,
+           hipStream_t st, hipStream_t back_st);
 }  // namespace pesq
 }  // namespace fsem

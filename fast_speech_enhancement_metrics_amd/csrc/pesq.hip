@@ -9,7 +9,8 @@
 // pesq_front  persistent 256-thread workgroups over items (signal, segment of 48 frames):
 //   A  float4 buffer loads of a 13 312-sample tile (768 warm-up + 48 hops + 1 hop) into LDS,
 //      prefetched in registers during the previous item's FFT phase
-//   J  (joint entry only) STOI's 16 -> 10 kHz resampler on the same tile (see resample_tile)
+//   J  (joint entry only) STOI's 16 -> 10 kHz resampler on the same tile, on MFMA, plus the
+//      STOI VAD quarter sums of the clean rows (see resample_tile)
 //   B  level-alignment band-pass power (PESQ.py:92-98), time-parallel:
 //        lane j owns chunk j (52 samples); end state of its zero-state response is a
 //        linear functional of the chunk (table kScanG); a 4-level Hillis-Steele scan with the
@@ -36,6 +37,7 @@
 
 #include "fsem_fft.h"
 #include "fsem_internal.h"
+#include "fsem_vad.h"
 
 namespace fsem {
 
@@ -225,64 +227,106 @@ __device__ __forceinline__ float iir_pass2(float4 *__restrict__ w4, float z[NS],
 // 10 kHz length), i.e. polyphase groups m = g*OWN/8 + j whose 28 taps x[8m - 10 + t] sit at
 // tile[WARM - 10 + 8j + t]; same tap order as stoi_resample_vad16, so bitwise the same y10.
 constexpr int OWN10 = OWN / 8 * 5;  // 7680
-constexpr int TILE_PAD = 16;        // zeros after the tile: the last segment's final taps
+constexpr int TILE_PAD = 32;        // zeros after the tile: the last segment's final taps
 static_assert(OWN % 8 == 0, "segments start on polyphase-group boundaries");
 static_assert((WARM - 12) % 4 == 0, "16-byte aligned tap reads");
-static_assert(WARM - 12 + 8 * ((TILE - WARM) * 5 / 8 / 5 - 1) + 32 <= TILE + TILE_PAD, "tap reads stay in the pad");
 
-// Each lane resamples RS_RUN consecutive groups from one sliding window of taps (8 new inputs
-// per further group), so a wave step covers 64 * RS_RUN groups: 16 tap reads per group instead
-// of 28, and lane windows 96 B apart (two-way b128 bank pattern).  Outputs are staged in the
-// wave's slice of the (then idle) exchange buffer and leave as aligned float4 stores.
-constexpr int RS_RUN = 3;
-constexpr int RS_STAGE = 64 * RS_RUN * 5;  // outputs per wave step
+// The polyphase resampler as a matrix product on MFMA (v_mfma_f32_16x16x4_f32).  Three
+// consecutive polyphase groups form a super-group: 24 inputs -> 15 outputs over 44 taps,
+//   y[15 s + p] = sum_{t<44} x[24 s - 10 + t] * R[t][p],
+//   R[t][p] = kRs16k10k[p % 5][t - 8 (p / 5)] (zero outside the 28 taps),
+// so a wave step multiplies A = the tile's Hankel rows of 64 super-groups (4 MFMA tiles of 16,
+// one tap per lane per K-step, read straight from the tile) by the constant B = R (11 K-steps
+// x 16 columns, column 15 zero; one VGPR per K-step, loaded once per kernel).  The f32 MFMA is
+// bit-for-bit a k-ordered fmaf chain and the zero taps add exact zeros, so every output is the
+// scalar resampler's fmaf chain over t = 0..27: the 10 kHz rows stay bitwise those of
+// stoi_resample_vad16.  The VALU stays free for the other workgroup on the SIMD.  Outputs are
+// staged output-major in the wave's slice of the (then idle) exchange buffer and leave as
+// aligned float4 stores.
+constexpr int RS_KS = 11;                  // K-steps (44 taps)
+constexpr int RS_TILES = 4;                // 16-super-group MFMA tiles per wave step
+constexpr int RS_STAGE = RS_TILES * 16 * 15;  // outputs per wave step (960)
 static_assert(4 * RS_STAGE <= XBUF, "resampler staging fits the exchange buffer");
-__device__ __forceinline__ void resample_tile(const float *__restrict__ tile, int64_t o_lo, int64_t o_hi,
-                                              float *__restrict__ yrow, float *__restrict__ stage, int lane,
-                                              int wave) {
-  const int ngrp = (int)((o_hi - o_lo + 4) / 5);
-  // opaque staging indices RS_RUN*5*lane + jj: adjacent stores would seed the SLP vectorizer,
-  // which pairs the five FMA chains into packed FMAs with SGPR coefficient pairs (SGPR spills)
-  int sidx[5];
-#pragma unroll
-  for (int jj = 0; jj < 5; ++jj) {
-    sidx[jj] = RS_RUN * 5 * lane + jj;
-    asm volatile("" : "+v"(sidx[jj]));
-  }
-  for (int st = 0;; ++st) {
-    const int g0 = 64 * RS_RUN * (4 * st + wave);  // first group of this wave step (uniform)
-    if (g0 >= ngrp) break;
-    // groups past ngrp read whatever follows (in the LDS allocation) and are never stored
-    const float4 *x4 = reinterpret_cast<const float4 *>(tile + (WARM - 12) + 8 * (g0 + RS_RUN * lane));
-    float v[8 * RS_RUN + 24];
-#pragma unroll
-    for (int q = 0; q < 2 * RS_RUN + 6; ++q) {
-      const float4 f = x4[q];
-      v[4 * q] = f.x;
-      v[4 * q + 1] = f.y;
-      v[4 * q + 2] = f.z;
-      v[4 * q + 3] = f.w;
+static_assert(OWN10 % RS_STAGE == 0 && OWN10 / RS_STAGE == 8, "two wave steps per wave and segment");
+// the last segment owns up to (TILE - WARM) * 5 / 8 outputs; the taps of its last super-group
+// (x 0 coefficients included: a NaN there would poison the row) stay in the zeroed pad.  Rows
+// past the outputs only feed their own (unstored) output rows.
+static_assert(WARM - 10 + 24 * (((TILE - WARM) * 5 / 8 + 14) / 15 - 1) + 4 * RS_KS <= TILE + TILE_PAD,
+              "tap reads of stored outputs stay in the tile");
+struct RsMfmaB {
+  float b[RS_KS][64];
+};
+constexpr RsMfmaB make_rs_b() {
+  RsMfmaB t{};
+  for (int ks = 0; ks < RS_KS; ++ks)
+    for (int l = 0; l < 64; ++l) {
+      const int k = 4 * ks + (l >> 4), p = l & 15, q = k - 8 * (p / 5);
+      t.b[ks][l] = (p < 15 && q >= 0 && q < 28) ? kRs16k10k[p % 5][q] : 0.f;
     }
+  return t;
+}
+__constant__ static const RsMfmaB kRsMfmaB = make_rs_b();
+
+// With vrow (clean rows of the joint entry), the staged outputs also give the STOI VAD quarter
+// sums of every complete 64-sample block (fsem_vad.h), so no kernel re-reads the 10 kHz rows for
+// the frame energies.
+__device__ __forceinline__ void resample_tile(const float *__restrict__ tile, int64_t o_lo, int64_t o_hi,
+                                              float *__restrict__ yrow, float2 *__restrict__ vrow,
+                                              float4 wa, float4 wb, const float rb[RS_KS],
+                                              float *__restrict__ stage, int lane, int wave) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  const int nsg = (int)((o_hi - o_lo + 14) / 15);  // super-groups holding outputs
+  const int row = lane & 15, kq = lane >> 4;
+  for (int st = 0;; ++st) {
+    const int s0 = 16 * RS_TILES * (4 * st + wave);  // first super-group of this wave step (uniform)
+    if (s0 >= nsg) break;
+    // A operand: lane (row, kq) holds x[24 s - 10 + 4 ks + kq] of super-group s = s0 + 16 tl + row;
+    // super-groups past nsg read tile samples (zeros past the row end) and are never stored
+    const float *__restrict__ a = tile + (WARM - 10) + 24 * (s0 + row) + kq;
+    f4 c[RS_TILES];
 #pragma unroll
-    for (int k = 0; k < RS_RUN; ++k) {
+    for (int tl = 0; tl < RS_TILES; ++tl) c[tl] = (f4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int jj = 0; jj < 5; ++jj) {
-        float acc = 0.f;
+    for (int ks = 0; ks < RS_KS; ++ks) {
+      float av[RS_TILES];
 #pragma unroll
-        for (int t = 0; t < 28; ++t) acc = fmaf(kRs16k10k[jj][t], v[8 * k + t + 2], acc);
-        // output-major staging: stride-15 dword writes are conflict-free (gcd(15, 64) = 1)
-        stage[sidx[jj] + 5 * k] = acc;
-      }
+      for (int tl = 0; tl < RS_TILES; ++tl) av[tl] = a[24 * 16 * tl + 4 * ks];
+#pragma unroll
+      for (int tl = 0; tl < RS_TILES; ++tl) c[tl] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[tl], rb[ks], c[tl], 0, 0, 0);
+    }
+    // D layout: lane holds rows 4 kq + i (super-groups), column row (output phase p < 15)
+    if (row < 15) {
+#pragma unroll
+      for (int tl = 0; tl < RS_TILES; ++tl)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) stage[15 * (16 * tl + 4 * kq + i) + row] = c[tl][i];
     }
     wave_lds_fence();
-    const int64_t ob = o_lo + 5 * (int64_t)g0;  // multiple of 4: aligned float4 stores
+    const int64_t ob = o_lo + 15 * (int64_t)s0;  // multiple of 64: aligned float4 stores, whole blocks
     const int n = (int)min((int64_t)RS_STAGE, o_hi - ob);
     const float4 *__restrict__ s4 = reinterpret_cast<const float4 *>(stage);
-    for (int q = lane; 4 * q < n; q += 64) {
-      if (4 * q + 3 < n) {
-        reinterpret_cast<float4 *>(yrow + ob)[q] = s4[q];
-      } else {
-        for (int c = 4 * q; c < n; ++c) yrow[ob + c] = stage[c];
+    if (vrow) {  // uniform: every lane runs every pass (the quarter sums shuffle over 16 lanes)
+      for (int q0 = 0; 4 * q0 < n; q0 += 64) {
+        const int q = q0 + lane;
+        // reads past n stay inside xbuf (4 * 256 floats from the last wave's slice) and only
+        // feed blocks that are not stored
+        const float4 v = s4[q];
+        if (4 * q + 3 < n) {
+          reinterpret_cast<float4 *>(yrow + ob)[q] = v;
+        } else {
+          for (int c = 4 * q; c < n; ++c) yrow[ob + c] = stage[c];
+        }
+        const float e = vad_quarter(v, wa, wb, lane);
+        if ((lane & 14) == 0 && 4 * (q & ~15) + 64 <= n)
+          reinterpret_cast<float *>(vrow)[2 * ((ob >> 6) + (q >> 4)) + (lane & 1)] = e;
+      }
+    } else {
+      for (int q = lane; 4 * q < n; q += 64) {
+        if (4 * q + 3 < n) {
+          reinterpret_cast<float4 *>(yrow + ob)[q] = s4[q];
+        } else {
+          for (int c = 4 * q; c < n; ++c) yrow[ob + c] = stage[c];
+        }
       }
     }
     wave_lds_fence();
@@ -295,7 +339,8 @@ template <bool JOINT, bool VARLEN>
 __global__ void __launch_bounds__(PT, 2)
     pesq_front(const float *__restrict__ ref, const float *__restrict__ deg, int64_t B, int64_t Lcap,
                int64_t ld, const int32_t *__restrict__ lens_arg, int F, int npseg, int nseg, int64_t nitems,
-               float *__restrict__ bark, float *__restrict__ ppart, float *__restrict__ y10, int64_t y_ld) {
+               float *__restrict__ bark, float *__restrict__ ppart, float *__restrict__ y10, int64_t y_ld,
+               float2 *__restrict__ vad, int64_t v_ld) {
   __shared__ __attribute__((aligned(16))) float tile[TILE + TILE_PAD];
   __shared__ __attribute__((aligned(16))) float xbuf[XBUF];
   __shared__ float red[8];
@@ -322,6 +367,18 @@ __global__ void __launch_bounds__(PT, 2)
     bhi_c[t] = band < NBARK ? kBandEdge[band + 1] : 0;
     bcor_c[t] = band < NBARK ? kBarkCorr[band] : 0.f;
   }
+
+  // VAD window quarters (joint entry): a wave step's chunk starts at 10 kHz sample
+  // g * OWN10 + 960 (4 st + wave), i.e. at quarter block 120 g + 15 (4 st + wave), so the block
+  // parity of this lane's group is (wave + lane / 16) & 1 for every step.  Loaded once: a
+  // load inside the step would wait (vmcnt) for the step's own y10 stores.
+  static_assert(OWN10 % 128 == 0 && RS_STAGE % 64 == 0 && (RS_STAGE / 64) % 2 == 1, "VAD block parity");
+  static_assert(RS_STAGE % 15 == 0, "wave steps start on super-group boundaries");
+  float4 vwa, vwb;
+  vad_windows(lane, (wave + (lane >> 4)) & 1, vwa, vwb);
+  float rsb[RS_KS];  // resampler MFMA B operand (this lane's column of R per K-step)
+#pragma unroll
+  for (int ks = 0; ks < RS_KS; ++ks) rsb[ks] = JOINT ? kRsMfmaB.b[ks][lane] : 0.f;
 
   float4 pre[PF];
   int64_t item = blockIdx.x;
@@ -367,13 +424,15 @@ __global__ void __launch_bounds__(PT, 2)
       }
     }
     lds_barrier();
+    STAMP(14);
     if (JOINT) {
       const int64_t L10 = (5 * L + 7) / 8;
       const int64_t o_lo = (int64_t)it.g * OWN10;
       const int64_t o_hi = (it.g == rg.nseg - 1) ? L10 : min(L10, o_lo + OWN10);
       const int64_t b = it.s < B ? it.s : it.s - B;
-      resample_tile(tile, o_lo, o_hi, y10 + (2 * b + (it.s < B ? 0 : 1)) * y_ld, xbuf + RS_STAGE * wave, lane,
-                    wave);
+      float2 *vrow = (vad && it.s < B) ? vad + b * v_ld : nullptr;  // clean rows only
+      resample_tile(tile, o_lo, o_hi, y10 + (2 * b + (it.s < B ? 0 : 1)) * y_ld, vrow, vwa, vwb, rsb,
+                    xbuf + RS_STAGE * wave, lane, wave);
     }
     STAMP(1);
     const int g = it.g;
@@ -818,7 +877,7 @@ extern "C" size_t fsem_pesq_workspace_bytes(int64_t batch, int64_t length) {
 
 int fsem::pesq::launch_front(const float *ref, const float *deg, int64_t batch, int64_t length, int64_t ld,
                              const int32_t *lengths, float *bark, float *power, void *ws, size_t ws_bytes,
-                             float *y10, int64_t y_ld, hipStream_t st) {
+                             float *y10, int64_t y_ld, float2 *vad, int64_t v_ld, hipStream_t st) {
   if (!ref || !deg || !bark || !power || batch <= 0 || length <= 0 || ld < length) return FSEM_EINVAL;
   const pesq::Geometry g = pesq::geometry(length);
   if (g.F < 20 && !lengths) return FSEM_ESHORT;
@@ -830,7 +889,7 @@ int fsem::pesq::launch_front(const float *ref, const float *deg, int64_t batch, 
   float *ppart = static_cast<float *>(ws);
 #define FSEM_FRONT(J, V)                                                                                \
   hipLaunchKernelGGL((pesq::pesq_front<J, V>), dim3((unsigned)grid), dim3(pesq::PT), 0, st, ref, deg, batch, \
-                     length, ld, lengths, g.F, g.npseg, g.nseg, nitems, bark, ppart, y10, y_ld)
+                     length, ld, lengths, g.F, g.npseg, g.nseg, nitems, bark, ppart, y10, y_ld, vad, v_ld)
   if (y10) {
     if (lengths) FSEM_FRONT(true, true);
     else FSEM_FRONT(true, false);
@@ -849,16 +908,18 @@ int fsem::pesq::launch_front(const float *ref, const float *deg, int64_t batch, 
 extern "C" int fsem_pesq_front_f32(const float *ref, const float *deg, int64_t batch, int64_t length,
                                    int64_t ld, const int32_t *lengths, float *bark, float *power, void *ws,
                                    size_t ws_bytes, void *stream) {
-  return pesq::launch_front(ref, deg, batch, length, ld, lengths, bark, power, ws, ws_bytes, nullptr, 0,
-                            (hipStream_t)stream);
+  return pesq::launch_front(ref, deg, batch, length, ld, lengths, bark, power, ws, ws_bytes, nullptr, 0, nullptr,
+                            0, (hipStream_t)stream);
 }
 
 extern "C" int fsem_pesq_front_y10_f32(const float *ref, const float *deg, int64_t batch, int64_t length,
                                        int64_t ld, const int32_t *lengths, float *bark, float *power, float *y10,
-                                       int64_t y_ld, void *ws, size_t ws_bytes, void *stream) {
+                                       int64_t y_ld, float *vad, int64_t vad_ld, void *ws, size_t ws_bytes,
+                                       void *stream) {
   if (!y10 || y_ld < (5 * length + 7) / 8 || (y_ld & 3)) return FSEM_EINVAL;
+  if (vad && vad_ld < fsem::vad_ld((5 * length + 7) / 8)) return FSEM_EINVAL;
   return pesq::launch_front(ref, deg, batch, length, ld, lengths, bark, power, ws, ws_bytes, y10, y_ld,
-                            (hipStream_t)stream);
+                            reinterpret_cast<float2 *>(vad), vad_ld, (hipStream_t)stream);
 }
 
 extern "C" size_t fsem_pesq_back_workspace_bytes(int64_t batch, int64_t length) {
@@ -908,7 +969,7 @@ int fsem::stream_wait(hipStream_t waiter, hipStream_t producer) {
 
 int fsem::pesq::run_wb(const float *ref, const float *deg, int64_t batch, int64_t length, int64_t ld,
                        const int32_t *lengths, float *mos, void *ws, size_t ws_bytes, float *y10, int64_t y_ld,
-                       hipStream_t stream, hipStream_t back_st) {
+                       float2 *vad, int64_t v_ld, hipStream_t stream, hipStream_t back_st) {
   if (!ref || !deg || !mos || batch <= 0 || length <= 0 || ld < length) return FSEM_EINVAL;
   const pesq::Geometry g = pesq::geometry(length);
   if (g.F < 20 && !lengths) return FSEM_ESHORT;
@@ -919,7 +980,8 @@ int fsem::pesq::run_wb(const float *ref, const float *deg, int64_t batch, int64_
   p += front + align_up(sizeof(float) * (size_t)(2 * batch) * (size_t)g.F * pesq::NBARK, 256);
   float *power = reinterpret_cast<float *>(p);
   p += align_up(sizeof(float) * (size_t)(2 * batch), 256);
-  int rc = pesq::launch_front(ref, deg, batch, length, ld, lengths, bark, power, ws, front, y10, y_ld, stream);
+  int rc = pesq::launch_front(ref, deg, batch, length, ld, lengths, bark, power, ws, front, y10, y_ld, vad, v_ld,
+                              stream);
   if (rc != FSEM_OK) return rc;
   rc = stream_wait(back_st, stream);
   if (rc != FSEM_OK) return rc;
@@ -930,6 +992,6 @@ int fsem::pesq::run_wb(const float *ref, const float *deg, int64_t batch, int64_
 extern "C" int fsem_pesq_wb_f32(const float *ref, const float *deg, int64_t batch, int64_t length,
                                 int64_t ld, const int32_t *lengths, float *mos, void *ws, size_t ws_bytes,
                                 void *stream) {
-  return pesq::run_wb(ref, deg, batch, length, ld, lengths, mos, ws, ws_bytes, nullptr, 0, (hipStream_t)stream,
-                       (hipStream_t)stream);
+  return pesq::run_wb(ref, deg, batch, length, ld, lengths, mos, ws, ws_bytes, nullptr, 0, nullptr, 0,
+                       (hipStream_t)stream, (hipStream_t)stream);
 }

@@ -6,11 +6,11 @@
 // into the kernels that consume the 10 kHz signal, so the resampled signal never exists
 // in HBM.  Four kernels per call:
 //
-//  stoi_vad      per (utterance, 64 VAD frames): resample the clean signal on the fly,
-//                frame energies of hann(257)[1:]-windowed 256-sample frames, hop 128, in dB
-//                (STOI.py:92-99).  Energy of frame i = P[i] + Q[i+1] over 128-sample blocks.
-//  stoi_select   per utterance: 40 dB voice-activity selection against the loudest clean
-//                frame, stream compaction of the kept frame indices (STOI.py:101-108).
+//  stoi_*vad*    resample the signals to 10 kHz (fused, or the joint PESQ front end does it) and
+//                the clean rows' VAD quarter sums: energies of hann(257)[1:]-windowed 256-sample
+//                frames, hop 128 (STOI.py:92-99), assembled from 64-sample blocks (fsem_vad.h).
+//  stoi_select   per utterance: frame energies in dB, 40 dB voice-activity selection against the
+//                loudest clean frame, stream compaction of the kept frame indices (STOI.py:101-108).
 //  stoi_tob      per (utterance, 32 STFT frames): overlap-added signal built directly from
 //                the kept frames (STOI.py:71-86, never materialised), 512-point FFT of
 //                clean + i*denoised (one wave per frame pair), 15 one-third-octave band
@@ -23,6 +23,7 @@
 #include "fsem_fft.h"
 #include "fsem_internal.h"
 #include "fsem_resample.h"
+#include "fsem_vad.h"
 
 namespace fsem {
 namespace stoi {
@@ -65,6 +66,24 @@ __device__ __forceinline__ float sample10(const Src &s, int64_t o, int64_t L10, 
   return direct ? s.x[o] : resample_at(s.x, s.n, o, rk);
 }
 
+// VAD quarter sums (fsem_vad.h) of the complete 64-sample blocks among the first n samples of
+// a 4096-sample chunk y (16-byte aligned; LDS or global), chunk start a multiple of 128 (block
+// parity = block index parity).  256 threads: 16 groups of 16 lanes, one block per group and pass
+// (block j = 16 pass + group: parity of the group index).  wa, wb = vad_windows(lane,
+// (tid >> 4) & 1), loaded by the caller up front (a load here would wait for its stores).
+__device__ __forceinline__ void vad_chunk(const float *__restrict__ y, int n, float2 *__restrict__ vrow, int tid,
+                                          float4 wa, float4 wb) {
+  const int lane = tid & 63, grp = tid >> 4;
+  const float4 *__restrict__ y4 = reinterpret_cast<const float4 *>(y);
+  for (int j0 = 0; 64 * j0 < n; j0 += 16) {  // uniform trip count: whole groups shuffle together
+    const int j = j0 + grp;
+    const bool full = 64 * j + 64 <= n;
+    const float4 v = full ? y4[16 * j + (lane & 15)] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float e = vad_quarter(v, wa, wb, lane);
+    if ((lane & 14) == 0 && full) reinterpret_cast<float *>(vrow)[2 * j + (lane & 1)] = e;
+  }
+}
+
 // Resample both signals of an utterance to 10 kHz once (written to the workspace, read back
 // only for the kept frames by stoi_tob) and compute the clean frame energies (STOI.py:92-99).
 // Persistent workgroups walk items (utterance, chunk, signal); the next item's 16 kHz input is
@@ -79,7 +98,7 @@ constexpr int XPF = (XT4 + 255) / 256;         // prefetch float4s per thread
 __global__ void __launch_bounds__(256, 2)
     stoi_resample_vad16(const float *__restrict__ ref, const float *__restrict__ deg, Rows rows, int64_t ld,
                         int nchunk, int64_t nitems, float *__restrict__ y10, int64_t y_ld,
-                        float *__restrict__ energy, int nv_ld) {
+                        float2 *__restrict__ vad, int64_t v_ld) {
   __shared__ __attribute__((aligned(16))) float xin[XPF * 256 * 4 + 4];
   __shared__ __attribute__((aligned(16))) float ytile[YT + 8];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -120,6 +139,8 @@ __global__ void __launch_bounds__(256, 2)
       pre[k] = make_float4(v.x, v.y, v.z, v.w);
     }
   };
+  float4 vwa, vwb;
+  vad_windows(lane, (tid >> 4) & 1, vwa, vwb);
   float4 pre[XPF];
   int64_t item = blockIdx.x;
   if (item < nitems) prefetch(item, pre);
@@ -132,7 +153,6 @@ __global__ void __launch_bounds__(256, 2)
       if (item + gridDim.x < nitems) prefetch(item + gridDim.x, pre);
       continue;
     }
-    const int NV = rows.nv(b);
     // staged at +2 floats: group m's 28 taps then start 16-byte aligned at xin[8(m - m0) + 4]
     float2 *x2 = reinterpret_cast<float2 *>(xin + 2);
 #pragma unroll
@@ -176,22 +196,7 @@ __global__ void __launch_bounds__(256, 2)
         for (int c = 4 * k; c < nown; ++c) yr[c] = ytile[c];
       }
     }
-    if (sig == 0) {
-      // frame energies 20 log10(||w * frame|| + 1e-9) (STOI.py:92-99)
-      for (int f = wave; f < VF2; f += 4) {
-        const int i = chunk * VF2 + f;
-        if (i >= NV) break;
-        const float *fr = ytile + 128 * f;
-        float acc = 0.f;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float v = kHann256s[lane + 64 * r] * fr[lane + 64 * r];
-          acc = fmaf(v, v, acc);
-        }
-        acc = wave_sum(acc);
-        if (lane == 0) energy[b * nv_ld + i] = 20.f * log10f(sqrtf(acc) + 1e-9f);
-      }
-    }
+    if (sig == 0) vad_chunk(ytile, nown, vad + b * v_ld + (o0 >> 6), tid, vwa, vwb);  // clean VAD quarter sums
     lds_barrier();
   }
 }
@@ -202,72 +207,47 @@ constexpr int YT3 = VF3 * 128 + 128;
 __global__ void __launch_bounds__(256)
     stoi_resample_vad(const float *__restrict__ ref, const float *__restrict__ deg, Rows rows, int64_t ld,
                       int mode, ResampleKernel rk, float *__restrict__ y10, int64_t y_ld,
-                      float *__restrict__ energy, int nv_ld) {
+                      float2 *__restrict__ vad, int64_t v_ld) {
   __shared__ __attribute__((aligned(16))) float ytile[YT3];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar branches)
   const int64_t b = blockIdx.y;
   const int64_t o0 = (int64_t)blockIdx.x * (VF3 * 128);
   const int64_t n_in = rows.n(b), L10 = rows.l10(b);
-  const int NV = rows.nv(b);
   if (o0 >= L10) return;
   const int64_t o_end = min(o0 + (int64_t)YT3, L10);
   const int ny = (int)(o_end - o0);
   const int nw_own = (int)min((int64_t)(VF3 * 128), L10 - o0);
+  float4 vwa, vwb;
+  vad_windows(lane, (tid >> 4) & 1, vwa, vwb);
   for (int sig = 0; sig < 2; ++sig) {
     const Src src{(sig == 0 ? ref : deg) + b * ld, n_in};
     for (int k = tid; k < ny; k += 256) ytile[k] = sample10(src, o0 + k, L10, mode == 1, rk);
     lds_barrier();
     float *__restrict__ yr = y10 + (b * 2 + sig) * y_ld + o0;
     for (int k = tid; k < nw_own; k += 256) yr[k] = ytile[k];
-    if (sig == 0) {
-      for (int f = wave; f < VF3; f += 4) {
-        const int i = blockIdx.x * VF3 + f;
-        if (i >= NV) break;
-        const float *fr = ytile + 128 * f;
-        float acc = 0.f;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float v = kHann256s[lane + 64 * r] * fr[lane + 64 * r];
-          acc = fmaf(v, v, acc);
-        }
-        acc = wave_sum(acc);
-        if (lane == 0) energy[b * nv_ld + i] = 20.f * log10f(sqrtf(acc) + 1e-9f);
-      }
-    }
+    if (sig == 0) vad_chunk(ytile, nw_own, vad + b * v_ld + (o0 >> 6), tid, vwa, vwb);
     lds_barrier();
   }
 }
 
-// Joint mode: the 10 kHz rows were written by pesq_front<true>; clean frame energies
-// (STOI.py:92-99) from them, one wave per frame, same arithmetic order as the fused kernels.
-constexpr int VFE = 64;  // VAD frames per workgroup
+// 10 kHz rows already in HBM (other-rate path: tiled resampler output): the clean rows' VAD
+// quarter sums, 4096 samples per workgroup.
+constexpr int VQ = 4096;
 __global__ void __launch_bounds__(256)
-    stoi_vad10(const float *__restrict__ y10, int64_t y_ld, Rows rows, float *__restrict__ energy, int nv_ld) {
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar branches)
+    stoi_vad10(const float *__restrict__ y10, int64_t y_ld, Rows rows, float2 *__restrict__ vad, int64_t v_ld) {
   const int64_t b = blockIdx.y;
-  const int NV = rows.nv(b);
-  const float *__restrict__ yc = y10 + (2 * b) * y_ld;
-  const float w0 = kHann256s[lane], w1 = kHann256s[lane + 64], w2 = kHann256s[lane + 128],
-              w3 = kHann256s[lane + 192];
-  for (int f = wave; f < VFE; f += 4) {
-    const int i = blockIdx.x * VFE + f;
-    if (i >= NV) break;
-    const float *fr = yc + 128 * (int64_t)i;
-    const float v0 = w0 * fr[lane], v1 = w1 * fr[lane + 64], v2 = w2 * fr[lane + 128], v3 = w3 * fr[lane + 192];
-    float acc = 0.f;
-    acc = fmaf(v0, v0, acc);
-    acc = fmaf(v1, v1, acc);
-    acc = fmaf(v2, v2, acc);
-    acc = fmaf(v3, v3, acc);
-    acc = wave_sum(acc);
-    if (lane == 0) energy[b * nv_ld + i] = 20.f * log10f(sqrtf(acc) + 1e-9f);
-  }
+  const int64_t o0 = (int64_t)blockIdx.x * VQ;
+  const int64_t L10 = rows.l10(b);
+  if (o0 >= L10) return;
+  float4 vwa, vwb;
+  vad_windows(threadIdx.x & 63, (threadIdx.x >> 4) & 1, vwa, vwb);
+  vad_chunk(y10 + (2 * b) * y_ld + o0, (int)min((int64_t)VQ, L10 - o0), vad + b * v_ld + (o0 >> 6), threadIdx.x, vwa,
+            vwb);
 }
 
 __global__ void __launch_bounds__(256)
-    stoi_select(const float *__restrict__ energy, int nv_ld, Rows rows, int *__restrict__ idx,
+    stoi_select(const float2 *__restrict__ vad, int64_t v_ld, int nv_ld, Rows rows, int *__restrict__ idx,
                 int *__restrict__ kept) {
   __shared__ float red[8];
   __shared__ int wcount[4];
@@ -275,15 +255,15 @@ __global__ void __launch_bounds__(256)
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar branches)
   const int64_t b = blockIdx.x;
   const int NV = rows.nv(b);
-  const float *e = energy + b * nv_ld;
+  const float2 *__restrict__ q = vad + b * v_ld;
   float m = -INFINITY;
-  for (int i = tid; i < NV; i += 256) m = fmaxf(m, e[i]);
+  for (int i = tid; i < NV; i += 256) m = fmaxf(m, vad_energy_db(q, i));
   m = block_max_256(m, red);
   const float thr = m - 40.f;  // (max - dynamic_range - e) < 0  (STOI.py:102)
   int base = 0;
   for (int i0 = 0; i0 < NV; i0 += 256) {
     const int i = i0 + tid;
-    const bool keep = (i < NV) && ((thr - e[i]) < 0.f);
+    const bool keep = (i < NV) && ((thr - vad_energy_db(q, i)) < 0.f);
     const unsigned long long bal = __ballot(keep);
     const int pre = __popcll(bal & ((1ull << lane) - 1ull));
     if (lane == 0) wcount[wave] = __popcll(bal);
@@ -536,6 +516,7 @@ __global__ void __launch_bounds__(SEG_T, 3)
 struct Geometry {
   int64_t L10;
   int NV, nv_ld, tmax;
+  int64_t v_ld;  // VAD quarter sums per row (float2)
   int64_t y_ld;
   bool direct;
   int mode;
@@ -555,6 +536,7 @@ inline int make_geometry(int64_t length, int32_t sr, Geometry *g, ResampleKernel
   }
   g->NV = g->L10 >= 256 ? (int)((g->L10 - 256) / 128 + 1) : 0;
   g->nv_ld = (int)align_up((size_t)(g->NV > 0 ? g->NV : 1), 64);
+  g->v_ld = vad_ld(g->L10);
   g->tmax = g->NV > 2 ? g->NV - 2 : 1;
   g->y_ld = (int64_t)align_up((size_t)g->L10, 64);
   g->mode = g->direct ? 1 : ((sr == 16000) ? 0 : 2);
@@ -563,7 +545,7 @@ inline int make_geometry(int64_t length, int32_t sr, Geometry *g, ResampleKernel
 
 inline size_t ws_bytes(int64_t B, const Geometry &g) {
   size_t s = 0;
-  s += align_up(sizeof(float) * (size_t)B * g.nv_ld, 256);                // energies
+  s += align_up(sizeof(float2) * (size_t)B * (size_t)g.v_ld, 256);        // VAD quarter sums
   s += align_up(sizeof(int) * (size_t)B * g.nv_ld, 256);                  // kept indices
   s += align_up(sizeof(int) * (size_t)B, 256);                            // kept counts
   s += align_up(sizeof(float) * (size_t)(2 * B) * NB * (size_t)g.tmax, 256);  // tob
@@ -573,7 +555,7 @@ inline size_t ws_bytes(int64_t B, const Geometry &g) {
 
 // Pointers into a STOI workspace laid out by ws_bytes().
 struct Ws {
-  float *energy;
+  float2 *vad;
   int *idx, *kept;
   float *tob, *y10;
 };
@@ -581,8 +563,8 @@ struct Ws {
 inline Ws carve(void *ws, int64_t B, const Geometry &g) {
   Ws w;
   char *p = static_cast<char *>(ws);
-  w.energy = reinterpret_cast<float *>(p);
-  p += align_up(sizeof(float) * (size_t)B * g.nv_ld, 256);
+  w.vad = reinterpret_cast<float2 *>(p);
+  p += align_up(sizeof(float2) * (size_t)B * (size_t)g.v_ld, 256);
   w.idx = reinterpret_cast<int *>(p);
   p += align_up(sizeof(int) * (size_t)B * g.nv_ld, 256);
   w.kept = reinterpret_cast<int *>(p);
@@ -594,9 +576,9 @@ inline Ws carve(void *ws, int64_t B, const Geometry &g) {
 }
 
 // Everything after the clean frame energies: selection, band envelopes, segments.
-inline int run_tail(int64_t B, const Geometry &g, const Rows &rows, const float *y10, const float *energy, int *idx,
+inline int run_tail(int64_t B, const Geometry &g, const Rows &rows, const float *y10, const float2 *vad, int *idx,
                     int *kept, float *tob, int64_t tmax, float *stoi_out, float *estoi_out, hipStream_t st) {
-  hipLaunchKernelGGL(stoi_select, dim3((unsigned)B), dim3(256), 0, st, energy, g.nv_ld, rows, idx, kept);
+  hipLaunchKernelGGL(stoi_select, dim3((unsigned)B), dim3(256), 0, st, vad, g.v_ld, g.nv_ld, rows, idx, kept);
   FSEM_CHECK_LAUNCH();
   hipLaunchKernelGGL(stoi_tob, dim3((unsigned)((g.tmax + TF - 1) / TF), (unsigned)B), dim3(256), 0, st, y10,
                      g.y_ld, B, rows, idx, kept, g.nv_ld, tob, tmax);
@@ -634,21 +616,21 @@ inline int run(const float *ref, const float *deg, int64_t B, int64_t length, in
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     const int64_t grid = nitems < (int64_t)ncu * 3 ? nitems : (int64_t)ncu * 3;  // 3 resident per CU
     hipLaunchKernelGGL(stoi_resample_vad16, dim3((unsigned)grid), dim3(256), 0, st, ref, deg, rows, ld, nchunk,
-                       nitems, w.y10, g.y_ld, w.energy, g.nv_ld);
+                       nitems, w.y10, g.y_ld, w.vad, g.v_ld);
   } else if (g.mode == 2) {
     // other rates: tiled polyphase resampler into the 10 kHz rows, then the clean energies
     rc = launch_resample_tiled(ref, B, length, ld, lengths, w.y10, 2 * g.y_ld, rk, st);
     if (rc != FSEM_OK) return rc;
     rc = launch_resample_tiled(deg, B, length, ld, lengths, w.y10 + g.y_ld, 2 * g.y_ld, rk, st);
     if (rc != FSEM_OK) return rc;
-    hipLaunchKernelGGL(stoi_vad10, dim3((unsigned)std::max(1, (g.NV + VFE - 1) / VFE), (unsigned)B), dim3(256), 0,
-                       st, w.y10, g.y_ld, rows, w.energy, g.nv_ld);
+    hipLaunchKernelGGL(stoi_vad10, dim3((unsigned)((g.L10 + VQ - 1) / VQ), (unsigned)B), dim3(256), 0, st, w.y10,
+                       g.y_ld, rows, w.vad, g.v_ld);
   } else {
     hipLaunchKernelGGL(stoi_resample_vad, dim3((unsigned)((g.L10 + VF3 * 128 - 1) / (VF3 * 128)), (unsigned)B),
-                       dim3(256), 0, st, ref, deg, rows, ld, g.mode, rk, w.y10, g.y_ld, w.energy, g.nv_ld);
+                       dim3(256), 0, st, ref, deg, rows, ld, g.mode, rk, w.y10, g.y_ld, w.vad, g.v_ld);
   }
   FSEM_CHECK_LAUNCH();
-  return run_tail(B, g, rows, w.y10, w.energy, w.idx, w.kept, w.tob, tmax, stoi_out, estoi_out, st);
+  return run_tail(B, g, rows, w.y10, w.vad, w.idx, w.kept, w.tob, tmax, stoi_out, estoi_out, st);
 }
 
 }  // namespace stoi
@@ -708,12 +690,10 @@ extern "C" int fsem_pesq_stoi_f32(const float *ref, const float *deg, int64_t ba
   // workgroup per pair, low occupancy) runs on a side stream concurrently with the STOI tail;
   // both only read what the front end wrote, and the caller's stream joins the side stream.
   const hipStream_t side = side_stream(st);
-  rc = pesq::run_wb(ref, deg, batch, length, ld, lengths, mos, ws, pesq_bytes, w.y10, g.y_ld, st, side);
+  rc = pesq::run_wb(ref, deg, batch, length, ld, lengths, mos, ws, pesq_bytes, w.y10, g.y_ld, w.vad, g.v_ld, st,
+                    side);
   if (rc != FSEM_OK) return rc;
-  hipLaunchKernelGGL(stoi::stoi_vad10, dim3((unsigned)std::max(1, (g.NV + stoi::VFE - 1) / stoi::VFE), (unsigned)batch),
-                     dim3(256), 0, st, w.y10, g.y_ld, rows, w.energy, g.nv_ld);
-  FSEM_CHECK_LAUNCH();
-  rc = stoi::run_tail(batch, g, rows, w.y10, w.energy, w.idx, w.kept, w.tob, g.tmax, stoi_out, estoi_out, st);
+  rc = stoi::run_tail(batch, g, rows, w.y10, w.vad, w.idx, w.kept, w.tob, g.tmax, stoi_out, estoi_out, st);
   const int rj = stream_wait(st, side);
   return rc != FSEM_OK ? rc : rj;
 }

@@ -89,11 +89,16 @@ int fsem_pesq_front_f32(const float *ref, const float *deg, int64_t batch, int64
 /* front_y10: the joint entry's front end -- as front, and also writes the rows' 10 kHz
  *        resampled signals (STOI's BaseMetric resampler, base.py:19-20) from the same tiles:
  *          y10 [2*batch, y_ld] float32, row 2b = clean b, 2b+1 = denoised b, first
- *          ceil(5*length_b/8) samples written; y_ld >= ceil(5*length/8), y_ld % 4 == 0.
+ *          ceil(5*length_b/8) samples written; y_ld >= ceil(5*length/8), y_ld % 4 == 0;
+ *          vad NULL or [batch, vad_ld, 2] float32: the clean rows' STOI voice-activity
+ *          quarter sums (remove_silent_frames' frame energies, STOI.py:92-99, per 64-sample
+ *          block m: {sum (w[64(m&1)+t] y[64m+t])^2, sum (w[128+64(m&1)+t] y[64m+t])^2}, w =
+ *          hann(257)[1:]) for every complete block; vad_ld >= floor(L10/64)+1 rounded up to 64.
  */
 int fsem_pesq_front_y10_f32(const float *ref, const float *deg, int64_t batch, int64_t length,
                             int64_t ld, const int32_t *lengths, float *bark, float *power,
-                            float *y10, int64_t y_ld, void *ws, size_t ws_bytes, void *stream);
+                            float *y10, int64_t y_ld, float *vad, int64_t vad_ld, void *ws,
+                            size_t ws_bytes, void *stream);
 size_t fsem_pesq_back_workspace_bytes(int64_t batch, int64_t length);
 int fsem_pesq_back_f32(const float *bark, const float *power, int64_t batch, int64_t length,
                        const int32_t *lengths, float *mos, void *ws, size_t ws_bytes,

@@ -228,7 +228,8 @@ def test_gpu_joint_api_list_of_dicts():
 @pytest.mark.gpu
 def test_gpu_front_y10_resampler_and_front_unchanged():
     """fsem_pesq_front_y10_f32: the 10 kHz rows match the reference's resampler (golden x10),
-    and bark / power are bitwise those of fsem_pesq_front_f32."""
+    the clean rows' VAD quarter sums match a float64 evaluation on those rows, and bark / power
+    are bitwise those of fsem_pesq_front_f32."""
     from fast_speech_enhancement_metrics_amd import _native
     lib = _native.load()
     g = load_golden("stoi_16k")
@@ -239,6 +240,8 @@ def test_gpu_front_y10_resampler_and_front_unchanged():
     F = lib.fsem_pesq_frames(L)
     L10 = (5 * L + 7) // 8
     y_ld = (L10 + 63) // 64 * 64
+    v_ld = (L10 // 64 + 1 + 63) // 64 * 64
+    vad = torch.full((B, v_ld, 2), float("nan"), device=dev)
     outs = []
     for joint in (False, True):
         bark = torch.full((2 * B, F, 49), -1.0, device=dev)
@@ -248,7 +251,8 @@ def test_gpu_front_y10_resampler_and_front_unchanged():
         h = _native.stream_handle(dev)
         if joint:
             rc = lib.fsem_pesq_front_y10_f32(c.data_ptr(), d.data_ptr(), B, L, L, None, bark.data_ptr(),
-                                             power.data_ptr(), y10.data_ptr(), y_ld, ws.data_ptr(), ws.numel(), h)
+                                             power.data_ptr(), y10.data_ptr(), y_ld, vad.data_ptr(), v_ld,
+                                             ws.data_ptr(), ws.numel(), h)
         else:
             rc = lib.fsem_pesq_front_f32(c.data_ptr(), d.data_ptr(), B, L, L, None, bark.data_ptr(),
                                          power.data_ptr(), ws.data_ptr(), ws.numel(), h)
@@ -258,8 +262,19 @@ def test_gpu_front_y10_resampler_and_front_unchanged():
     y = outs[1][2].cpu().numpy()
     np.testing.assert_allclose(y[0::2, :L10], g["x10_clean"], atol=2e-6, rtol=0)
     assert np.isfinite(y[1::2, :L10]).all()
+    # VAD quarter sums of every complete 64-sample block of the clean rows (fsem_vad.h)
+    w = torch.hann_window(257).numpy()[1:].astype(np.float64)
+    nq = L10 // 64
+    blocks = y[0::2, :64 * nq].astype(np.float64).reshape(B, nq, 64)
+    par = (np.arange(nq) & 1)[:, None] * 64 + np.arange(64)[None, :]
+    want = np.stack([((w[par] * blocks) ** 2).sum(-1), ((w[128 + par] * blocks) ** 2).sum(-1)], -1)
+    got = vad.cpu().numpy()[:, :nq]
+    np.testing.assert_allclose(got, want, rtol=2e-5, atol=1e-30)
     assert lib.fsem_pesq_front_y10_f32(c.data_ptr(), d.data_ptr(), B, L, L, None, c.data_ptr(), c.data_ptr(),
-                                       c.data_ptr(), L10 - 1, c.data_ptr(), 1 << 30, None) == -1
+                                       c.data_ptr(), L10 - 1, None, 0, c.data_ptr(), 1 << 30, None) == -1
+    assert lib.fsem_pesq_front_y10_f32(c.data_ptr(), d.data_ptr(), B, L, L, None, c.data_ptr(), c.data_ptr(),
+                                       c.data_ptr(), y_ld, c.data_ptr(), v_ld - 64, c.data_ptr(), 1 << 30,
+                                       None) == -1
 
 
 def test_joint_8k_cpu_mode_matches_reference():

@@ -26,7 +26,7 @@ fn = lib.fsem_debug_read_stamps
 fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
 assert fn(buf.ctypes.data, buf.nbytes) == 0
 st = buf.astype(np.float64)
-segs = [("tile->LDS (+resample)", 0, 1), ("IIR pass1", 1, 2), ("scan", 2, 3), ("IIR pass2", 3, 4),
+segs = [("tile->LDS", 0, 14), ("resample", 14, 1), ("IIR pass1", 1, 2), ("scan", 2, 3), ("IIR pass2", 3, 4),
         ("fft r0", 4, 6)] + [(f"fft r{r}", 5 + r, 6 + r) for r in range(1, 7)] + [("mfma bark", 13, 15)]
 valid = (st[:, 15] > 0) & (st[:, 0] > 0)
 tot = (st[valid, 15] - st[valid, 0]).mean()
