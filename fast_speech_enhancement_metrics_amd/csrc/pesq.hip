@@ -357,15 +357,37 @@ __global__ void __launch_bounds__(PT, 2)
   fft512_twiddles(lane, tw1, tw2);
   const int plane = (64 - lane) & 63;
   // Bark MFMA (v_mfma_f32_16x16x4_f32): wave w owns frame rows 16w..16w+15 of the segment and
-  // all four 16-band tiles; B operand = fbank x correction from per-lane band edges.
-  int blo_c[4], bhi_c[4];
-  float bcor_c[4];
+  // all four 16-band tiles; B operand = fbank x correction.  Per lane (band 16 t + lane % 16,
+  // bins 4 k + lane / 16 of K-step k) one bit per K-step of the tile's range says whether the
+  // bin lies in the band: tiles 0, 1, 3 (5 + 11 + 5 steps) share one word, tile 2 (45 steps)
+  // takes two.  B of step k = bcor & -(bit k): one bit-field extract and one AND.
+  constexpr int K0a = kBarkTileK[0][0], K0b = kBarkTileK[0][1];
+  constexpr int K1a = kBarkTileK[1][0], K1b = kBarkTileK[1][1];
+  constexpr int K2a = kBarkTileK[2][0], K2b = kBarkTileK[2][1];
+  constexpr int K3a = kBarkTileK[3][0], K3b = kBarkTileK[3][1];
+  static_assert((K0b - K0a) + (K1b - K1a) + (K3b - K3a) <= 32 && K2b - K2a <= 64, "Bark band masks");
+  uint32_t bm013_c = 0, bm2lo_c = 0, bm2hi_c = 0;
+  uint32_t bcor_c[4];
+  {
+    int blo[4], bhi[4];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int band = 16 * t + (lane & 15);
-    blo_c[t] = band < NBARK ? kBandEdge[band] : 0;
-    bhi_c[t] = band < NBARK ? kBandEdge[band + 1] : 0;
-    bcor_c[t] = band < NBARK ? kBarkCorr[band] : 0.f;
+    for (int t = 0; t < 4; ++t) {
+      const int band = 16 * t + (lane & 15);
+      blo[t] = band < NBARK ? kBandEdge[band] : 0;
+      bhi[t] = band < NBARK ? kBandEdge[band + 1] : 0;
+      bcor_c[t] = __float_as_uint(band < NBARK ? kBarkCorr[band] : 0.f);
+    }
+    auto in = [&](int t, int k) {
+      const int bin = 4 * k + (lane >> 4);
+      return bin >= blo[t] && bin < bhi[t];
+    };
+    for (int k = K0a; k < K0b; ++k) bm013_c |= (uint32_t)in(0, k) << (k - K0a);
+    for (int k = K1a; k < K1b; ++k) bm013_c |= (uint32_t)in(1, k) << (k - K1a + (K0b - K0a));
+    for (int k = K3a; k < K3b; ++k) bm013_c |= (uint32_t)in(3, k) << (k - K3a + (K0b - K0a) + (K1b - K1a));
+    for (int k = K2a; k < K2b; ++k) {
+      if (k - K2a < 32) bm2lo_c |= (uint32_t)in(2, k) << (k - K2a);
+      else bm2hi_c |= (uint32_t)in(2, k) << (k - K2a - 32);
+    }
   }
 
   // VAD window quarters (joint entry): a wave step's chunk starts at 10 kHz sample
@@ -508,6 +530,8 @@ __global__ void __launch_bounds__(PT, 2)
       const bool plain = own_lo <= 0 && own_hi >= CH && lim >= CH;
       if (__builtin_amdgcn_readfirstlane((int)wave_edge))
         acc = iir_pass2<true, true>(w4, z, own_lo, own_hi, lim, t_lane, L);
+      else if (__builtin_amdgcn_readfirstlane((int)__all(plain)))
+        acc = iir_pass2<false, false>(w4, z, own_lo, own_hi, lim, t_lane, L);
       else
         acc = iir_pass2<false, true>(w4, z, own_lo, own_hi, lim, t_lane, L);
       // per-wave partials (no workgroup barrier); pesq_power_sum adds them in a fixed order
@@ -549,8 +573,8 @@ __global__ void __launch_bounds__(PT, 2)
             mi = v[(8 - r) & 7].i;
           }
           const float zr = v[r].r, zi = v[r].i;
-          pa[r] = 0.25f * ((zr + mr) * (zr + mr) + (zi - mi) * (zi - mi));
-          pb[r] = 0.25f * ((zi + mi) * (zi + mi) + (zr - mr) * (zr - mr));
+          pa[r] = 0.25f * fmaf(zr + mr, zr + mr, (zi - mi) * (zi - mi));  // explicit: no contraction choice
+          pb[r] = 0.25f * fmaf(zi + mi, zi + mi, (zr - mr) * (zr - mr));
         }
         if (lane == 0) {  // spec[:, :, 0] = 0 (PESQ.py:136)
           pa[0] = 0.f;
@@ -578,23 +602,21 @@ __global__ void __launch_bounds__(PT, 2)
       const int row = lane & 15, kq = lane >> 4;
       const float *srow = tile + SPEC_LD * min(16 * wave + row, nfr - 1);
       f4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, c2a = c0, c2b = c0, c3 = c0;
-      // opaque copies: keep the 66 B-operand selects inside the item loop (else LICM hoists
+      // opaque copies: keep the 66 B-operand extracts inside the item loop (else LICM hoists
       // them all into live VGPRs across the whole kernel)
-      int blo[4], bhi[4];
-      float bcor[4];
+      uint32_t bm013 = bm013_c, bm2lo = bm2lo_c, bm2hi = bm2hi_c, bcor[4];
+      asm volatile("" : "+v"(bm013), "+v"(bm2lo), "+v"(bm2hi));
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        blo[t] = blo_c[t];
-        bhi[t] = bhi_c[t];
         bcor[t] = bcor_c[t];
-        asm volatile("" : "+v"(blo[t]), "+v"(bhi[t]), "+v"(bcor[t]));
+        asm volatile("" : "+v"(bcor[t]));
       }
+      // B operand of K-step bit `bit` of mask word w: bcor where the bit is set, else +0
+      auto bop = [](uint32_t w, int bit, uint32_t cor) {
+        return __uint_as_float(cor & (uint32_t)__builtin_amdgcn_sbfe((int)w, bit, 1));
+      };
       // A operand: the wave's 16 spectrum rows, one bin per lane per K-step; issue all LDS
       // reads of a tile before its MFMA chain (the chain then never waits on LDS latency)
-      constexpr int K0a = kBarkTileK[0][0], K0b = kBarkTileK[0][1];
-      constexpr int K1a = kBarkTileK[1][0], K1b = kBarkTileK[1][1];
-      constexpr int K2a = kBarkTileK[2][0], K2b = kBarkTileK[2][1];
-      constexpr int K3a = kBarkTileK[3][0], K3b = kBarkTileK[3][1];
       {
         float a0[K0b - K0a], a1[K1b - K1a], a3[K3b - K3a];
 #pragma unroll
@@ -604,20 +626,15 @@ __global__ void __launch_bounds__(PT, 2)
 #pragma unroll
         for (int k = 0; k < K3b - K3a; ++k) a3[k] = srow[4 * (K3a + k) + kq];
 #pragma unroll
-        for (int k = 0; k < K0b - K0a; ++k) {
-          const int bin = 4 * (K0a + k) + kq;
-          c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[k], (bin >= blo[0] && bin < bhi[0]) ? bcor[0] : 0.f, c0, 0, 0, 0);
-        }
+        for (int k = 0; k < K0b - K0a; ++k)
+          c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[k], bop(bm013, k, bcor[0]), c0, 0, 0, 0);
 #pragma unroll
-        for (int k = 0; k < K1b - K1a; ++k) {
-          const int bin = 4 * (K1a + k) + kq;
-          c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[k], (bin >= blo[1] && bin < bhi[1]) ? bcor[1] : 0.f, c1, 0, 0, 0);
-        }
+        for (int k = 0; k < K1b - K1a; ++k)
+          c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[k], bop(bm013, k + (K0b - K0a), bcor[1]), c1, 0, 0, 0);
 #pragma unroll
-        for (int k = 0; k < K3b - K3a; ++k) {
-          const int bin = 4 * (K3a + k) + kq;
-          c3 = __builtin_amdgcn_mfma_f32_16x16x4f32(a3[k], (bin >= blo[3] && bin < bhi[3]) ? bcor[3] : 0.f, c3, 0, 0, 0);
-        }
+        for (int k = 0; k < K3b - K3a; ++k)
+          c3 = __builtin_amdgcn_mfma_f32_16x16x4f32(a3[k], bop(bm013, k + (K0b - K0a) + (K1b - K1a), bcor[3]), c3,
+                                                     0, 0, 0);
       }
       constexpr int KB = 16;  // tile 2 in batches of 16 K-steps, two accumulators
 #pragma unroll
@@ -628,8 +645,8 @@ __global__ void __launch_bounds__(PT, 2)
 #pragma unroll
         for (int k = 0; k < KB; ++k) {
           if (k0 + k < K2b) {
-            const int bin = 4 * (k0 + k) + kq;
-            const float bv = (bin >= blo[2] && bin < bhi[2]) ? bcor[2] : 0.f;
+            const int j = k0 + k - K2a;
+            const float bv = j < 32 ? bop(bm2lo, j, bcor[2]) : bop(bm2hi, j - 32, bcor[2]);
             if (k & 1)
               c2b = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[k], bv, c2b, 0, 0, 0);
             else

@@ -359,8 +359,8 @@ __global__ void __launch_bounds__(256)
         mi = v[(8 - r) & 7].i;
       }
       const float zr = v[r].r, zi = v[r].i;
-      pc[r] = 0.25f * ((zr + mr) * (zr + mr) + (zi - mi) * (zi - mi));
-      pd[r] = 0.25f * ((zi + mi) * (zi + mi) + (zr - mr) * (zr - mr));
+      pc[r] = 0.25f * fmaf(zr + mr, zr + mr, (zi - mi) * (zi - mi));  // explicit: no contraction choice
+      pd[r] = 0.25f * fmaf(zi + mi, zi + mi, (zr - mr) * (zr - mr));
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
