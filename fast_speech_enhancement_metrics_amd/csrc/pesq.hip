@@ -188,37 +188,65 @@ __device__ __forceinline__ void iir_pass1(const float4 *__restrict__ my4, int64_
 
 // IIR pass 2 from the true start state z: band-pass cascade (power over owned samples) and
 // pre-emphasis, whose output overwrites the chunk in place (zero from `lim` on).
+// MASK: per-sample ownership / end-of-row masks (first / last segment of a row, edge waves).
+// Without MASK every sample is owned-or-not by whole 4-sample groups: a non-final segment's
+// owned range [WARM, WARM + OWN) cuts chunks only at chunk offsets P_LO = WARM % CH and
+// P_HI = (WARM + OWN) % CH, so the band-pass power is summed in three accumulators --
+// samples [0, P_HI), [P_HI, P_LO), [P_LO, CH) -- and each lane keeps the parts it owns.
+constexpr int P_HI = (WARM + OWN) % CH, P_LO = WARM % CH;
+static_assert(P_HI % 4 == 0 && P_LO % 4 == 0 && P_HI < P_LO, "pass-2 power split points");
+
 template <bool TAPER, bool MASK>
-__device__ __forceinline__ float iir_pass2(float4 *__restrict__ w4, float z[NS], int own_lo, int own_hi,
-                                           int lim, int64_t t_lane, int64_t L) {
+__device__ __forceinline__ void iir_pass2_group(float4 *__restrict__ w4, int q, float z[NS], float &acc, int own_lo,
+                                                int own_hi, int lim, float tf0, float Lf) {
   const float b0 = kPreB[0], b1 = kPreB[1], b2 = kPreB[2], a1 = kPreA[1], a2 = kPreA[2];
+  const float4 v = w4[q];
+  float xs[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int n = 4 * q + c;
+    float u = xs[c];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const float y = u + z[2 * k];
+      z[2 * k] = fmaf(-kBpSecA[k][0], y, z[2 * k + 1]);
+      z[2 * k + 1] = fmaf(-kBpSecA[k][1], y, -u);
+      u = y;
+    }
+    acc = (!MASK || (n >= own_lo && n < own_hi)) ? fmaf(u, u, acc) : acc;
+    const float xp = TAPER ? xs[c] * taper_w(tf0 + (float)n, Lf) : xs[c];
+    const float y = fmaf(b0, xp, z[NBP]);
+    z[NBP] = fmaf(b1, xp, fmaf(-a1, y, z[NBP + 1]));
+    z[NBP + 1] = fmaf(b2, xp, -a2 * y);
+    xs[c] = (!MASK || n < lim) ? y : 0.f;  // the reference zero-pads AFTER the filter (PESQ.py:128)
+  }
+  w4[q] = make_float4(xs[0], xs[1], xs[2], xs[3]);
+}
+
+template <bool TAPER>
+__device__ __forceinline__ float iir_pass2_masked(float4 *__restrict__ w4, float z[NS], int own_lo, int own_hi,
+                                                  int lim, int64_t t_lane, int64_t L) {
   const float tf0 = (float)t_lane, Lf = (float)L;
   float acc = 0.f;
 #pragma unroll 3
-  for (int q = 0; q < CH / 4; ++q) {
-    const float4 v = w4[q];
-    float xs[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int n = 4 * q + c;
-      float u = xs[c];
-#pragma unroll
-      for (int k = 0; k < 5; ++k) {
-        const float y = u + z[2 * k];
-        z[2 * k] = fmaf(-kBpSecA[k][0], y, z[2 * k + 1]);
-        z[2 * k + 1] = fmaf(-kBpSecA[k][1], y, -u);
-        u = y;
-      }
-      acc = (!MASK || (n >= own_lo && n < own_hi)) ? fmaf(u, u, acc) : acc;
-      const float xp = TAPER ? xs[c] * taper_w(tf0 + (float)n, Lf) : xs[c];
-      const float y = fmaf(b0, xp, z[NBP]);
-      z[NBP] = fmaf(b1, xp, fmaf(-a1, y, z[NBP + 1]));
-      z[NBP + 1] = fmaf(b2, xp, -a2 * y);
-      xs[c] = (!MASK || n < lim) ? y : 0.f;  // the reference zero-pads AFTER the filter (PESQ.py:128)
-    }
-    w4[q] = make_float4(xs[0], xs[1], xs[2], xs[3]);
-  }
+  for (int q = 0; q < CH / 4; ++q) iir_pass2_group<TAPER, true>(w4, q, z, acc, own_lo, own_hi, lim, tf0, Lf);
   return acc;
+}
+
+// Unmasked: the owned power of a lane whose range boundaries lie at 0, P_HI, P_LO or CH.
+__device__ __forceinline__ float iir_pass2_split(float4 *__restrict__ w4, float z[NS], int own_lo, int own_hi) {
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+#pragma unroll
+  for (int q = 0; q < P_HI / 4; ++q) iir_pass2_group<false, false>(w4, q, z, a0, 0, 0, 0, 0.f, 0.f);
+#pragma unroll 3
+  for (int q = P_HI / 4; q < P_LO / 4; ++q) iir_pass2_group<false, false>(w4, q, z, a1, 0, 0, 0, 0.f, 0.f);
+#pragma unroll
+  for (int q = P_LO / 4; q < CH / 4; ++q) iir_pass2_group<false, false>(w4, q, z, a2, 0, 0, 0, 0.f, 0.f);
+  const bool lo_in = own_lo <= 0, hi_in = own_hi >= CH;
+  return (lo_in && hi_in) ? (a0 + a1) + a2
+       : (own_lo == P_LO && hi_in) ? a2
+       : (lo_in && own_hi == P_HI) ? a0
+       : 0.f;
 }
 
 // Joint mode (fsem_pesq_stoi_f32): STOI's 16 -> 10 kHz resampler (BaseMetric.prepare_audio,
@@ -526,14 +554,16 @@ __global__ void __launch_bounds__(PT, 2)
       const int lim = (int)min((int64_t)CH, max((int64_t)0, L - t_lane));       // y = 0 from here
       float4 *w4 = reinterpret_cast<float4 *>(tile + CH * tid);
       float acc;
-      // masks are only needed where a wave's chunks straddle the owned range or L
-      const bool plain = own_lo <= 0 && own_hi >= CH && lim >= CH;
+      // per-sample masks only where a lane's owned range is cut elsewhere than at the split
+      // points (a row's last segment) or the row ends inside the chunk
+      const bool split_ok = (own_lo <= 0 || own_lo == P_LO || own_lo >= CH) &&
+                            (own_hi >= CH || own_hi == P_HI || own_hi <= 0) && lim >= CH;
       if (__builtin_amdgcn_readfirstlane((int)wave_edge))
-        acc = iir_pass2<true, true>(w4, z, own_lo, own_hi, lim, t_lane, L);
-      else if (__builtin_amdgcn_readfirstlane((int)__all(plain)))
-        acc = iir_pass2<false, false>(w4, z, own_lo, own_hi, lim, t_lane, L);
+        acc = iir_pass2_masked<true>(w4, z, own_lo, own_hi, lim, t_lane, L);
+      else if (__builtin_amdgcn_readfirstlane((int)__all(split_ok)))
+        acc = iir_pass2_split(w4, z, own_lo, own_hi);
       else
-        acc = iir_pass2<false, true>(w4, z, own_lo, own_hi, lim, t_lane, L);
+        acc = iir_pass2_masked<false>(w4, z, own_lo, own_hi, lim, t_lane, L);
       // per-wave partials (no workgroup barrier); pesq_power_sum adds them in a fixed order
       const float tot = wave_sum(acc);
       if (lane == 0) ppart[(it.s * nseg + g) * 4 + wave] = tot * (kBpGain * kBpGain);
