@@ -627,12 +627,13 @@ __global__ void __launch_bounds__(PT, 2)
     STAMP(13);
 
     // ---------------------------------------------------------------- Bark bands on MFMA
-    if (16 * wave < nfr) {
+    // Work split over the four waves (K-steps of v_mfma_f32_16x16x4_f32): waves 0-2 take frame
+    // tile f = wave with band tiles 2 (45 steps) and 0 (5); wave 3 takes band tiles 1 (11) and
+    // 3 (5) of all three frame tiles -- 50 / 48 MFMAs per wave instead of 66 on three waves.
+    {
       typedef float f4 __attribute__((ext_vector_type(4)));
       const int row = lane & 15, kq = lane >> 4;
-      const float *srow = tile + SPEC_LD * min(16 * wave + row, nfr - 1);
-      f4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, c2a = c0, c2b = c0, c3 = c0;
-      // opaque copies: keep the 66 B-operand extracts inside the item loop (else LICM hoists
+      // opaque copies: keep the B-operand extracts inside the item loop (else LICM hoists
       // them all into live VGPRs across the whole kernel)
       uint32_t bm013 = bm013_c, bm2lo = bm2lo_c, bm2hi = bm2hi_c, bcor[4];
       asm volatile("" : "+v"(bm013), "+v"(bm2lo), "+v"(bm2hi));
@@ -645,55 +646,88 @@ __global__ void __launch_bounds__(PT, 2)
       auto bop = [](uint32_t w, int bit, uint32_t cor) {
         return __uint_as_float(cor & (uint32_t)__builtin_amdgcn_sbfe((int)w, bit, 1));
       };
-      // A operand: the wave's 16 spectrum rows, one bin per lane per K-step; issue all LDS
-      // reads of a tile before its MFMA chain (the chain then never waits on LDS latency)
-      {
-        float a0[K0b - K0a], a1[K1b - K1a], a3[K3b - K3a];
+      auto brow_of = [&](int f) { return bark + ((int64_t)it.s * F + (int64_t)g * NF + 16 * f) * NBARK; };
+      if (wave < 3) {
+        if (16 * wave < nfr) {
+          const float *srow = tile + SPEC_LD * min(16 * wave + row, nfr - 1);
+          f4 c0 = {0.f, 0.f, 0.f, 0.f}, c2a = c0, c2b = c0;
+          // A operand: the wave's 16 spectrum rows, one bin per lane per K-step; a batch's LDS
+          // reads are issued before its MFMA chain (the chain then never waits on LDS latency)
+          {
+            float a0[K0b - K0a];
 #pragma unroll
-        for (int k = 0; k < K0b - K0a; ++k) a0[k] = srow[4 * (K0a + k) + kq];
+            for (int k = 0; k < K0b - K0a; ++k) a0[k] = srow[4 * (K0a + k) + kq];
 #pragma unroll
-        for (int k = 0; k < K1b - K1a; ++k) a1[k] = srow[4 * (K1a + k) + kq];
+            for (int k = 0; k < K0b - K0a; ++k)
+              c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[k], bop(bm013, k, bcor[0]), c0, 0, 0, 0);
+          }
+          constexpr int KB = 16;  // tile 2 in batches of 16 K-steps, two accumulators
 #pragma unroll
-        for (int k = 0; k < K3b - K3a; ++k) a3[k] = srow[4 * (K3a + k) + kq];
+          for (int k0 = K2a; k0 < K2b; k0 += KB) {
+            float a2[KB];
 #pragma unroll
-        for (int k = 0; k < K0b - K0a; ++k)
-          c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[k], bop(bm013, k, bcor[0]), c0, 0, 0, 0);
+            for (int k = 0; k < KB; ++k) a2[k] = (k0 + k < K2b) ? srow[4 * (k0 + k) + kq] : 0.f;
 #pragma unroll
-        for (int k = 0; k < K1b - K1a; ++k)
-          c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[k], bop(bm013, k + (K0b - K0a), bcor[1]), c1, 0, 0, 0);
+            for (int k = 0; k < KB; ++k) {
+              if (k0 + k < K2b) {
+                const int j = k0 + k - K2a;
+                const float bv = j < 32 ? bop(bm2lo, j, bcor[2]) : bop(bm2hi, j - 32, bcor[2]);
+                if (k & 1)
+                  c2b = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[k], bv, c2b, 0, 0, 0);
+                else
+                  c2a = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[k], bv, c2a, 0, 0, 0);
+              }
+            }
+          }
+          float *brow = brow_of(wave);
 #pragma unroll
-        for (int k = 0; k < K3b - K3a; ++k)
-          c3 = __builtin_amdgcn_mfma_f32_16x16x4f32(a3[k], bop(bm013, k + (K0b - K0a) + (K1b - K1a), bcor[3]), c3,
-                                                     0, 0, 0);
-      }
-      constexpr int KB = 16;  // tile 2 in batches of 16 K-steps, two accumulators
-#pragma unroll
-      for (int k0 = K2a; k0 < K2b; k0 += KB) {
-        float a2[KB];
-#pragma unroll
-        for (int k = 0; k < KB; ++k) a2[k] = (k0 + k < K2b) ? srow[4 * (k0 + k) + kq] : 0.f;
-#pragma unroll
-        for (int k = 0; k < KB; ++k) {
-          if (k0 + k < K2b) {
-            const int j = k0 + k - K2a;
-            const float bv = j < 32 ? bop(bm2lo, j, bcor[2]) : bop(bm2hi, j - 32, bcor[2]);
-            if (k & 1)
-              c2b = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[k], bv, c2b, 0, 0, 0);
-            else
-              c2a = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[k], bv, c2a, 0, 0, 0);
+          for (int i = 0; i < 4; ++i) {
+            if (16 * wave + 4 * kq + i < nfr) {
+              float *o = brow + (4 * kq + i) * NBARK;
+              o[row] = c0[i];
+              o[32 + row] = c2a[i] + c2b[i];
+            }
           }
         }
-      }
-      float *brow = bark + ((int64_t)it.s * F + (int64_t)g * NF + 16 * wave) * NBARK;
+      } else {
+        f4 c1[3], c3[3];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int fl = 16 * wave + 4 * kq + i;
-        if (fl < nfr) {
-          float *o = brow + (4 * kq + i) * NBARK;
-          o[row] = c0[i];
-          o[16 + row] = c1[i];
-          o[32 + row] = c2a[i] + c2b[i];
-          if (row == 0) o[48] = c3[i];
+        for (int f = 0; f < 3; ++f) {
+          c1[f] = (f4){0.f, 0.f, 0.f, 0.f};
+          c3[f] = c1[f];
+        }
+        // three frame tiles = three independent accumulator chains per band tile
+#pragma unroll
+        for (int f = 0; f < 3; ++f) {
+          if (16 * f < nfr) {
+            const float *srow = tile + SPEC_LD * min(16 * f + row, nfr - 1);
+            float a1[K1b - K1a], a3[K3b - K3a];
+#pragma unroll
+            for (int k = 0; k < K1b - K1a; ++k) a1[k] = srow[4 * (K1a + k) + kq];
+#pragma unroll
+            for (int k = 0; k < K3b - K3a; ++k) a3[k] = srow[4 * (K3a + k) + kq];
+#pragma unroll
+            for (int k = 0; k < K1b - K1a; ++k)
+              c1[f] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[k], bop(bm013, k + (K0b - K0a), bcor[1]), c1[f], 0, 0, 0);
+#pragma unroll
+            for (int k = 0; k < K3b - K3a; ++k)
+              c3[f] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                  a3[k], bop(bm013, k + (K0b - K0a) + (K1b - K1a), bcor[3]), c3[f], 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int f = 0; f < 3; ++f) {
+          if (16 * f < nfr) {
+            float *brow = brow_of(f);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              if (16 * f + 4 * kq + i < nfr) {
+                float *o = brow + (4 * kq + i) * NBARK;
+                o[16 + row] = c1[f][i];
+                if (row == 0) o[48] = c3[f][i];
+              }
+            }
+          }
         }
       }
     }
