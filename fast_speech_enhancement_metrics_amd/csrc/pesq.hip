@@ -77,6 +77,11 @@ static_assert(2 * PT * SCAN_LD <= XBUF, "double-buffered scan fits the exchange 
 static_assert(SPEC_LD * (NF - 1) + 256 <= TILE, "parked spectra stay in the tile");
 static_assert(TILE % (4 * PT) == 0, "prefetch split");
 
+// Bark bands are stored band-major per signal: bark[(s * NBARK + k) * bark_ld(F) + f], rows
+// padded to a multiple of 4 frames (aligned float4 stores from the MFMA tiles; the back end
+// reads one band of 64 consecutive frames per load, lane = frame).
+__host__ __device__ inline int64_t bark_ld(int F) { return (F + 3) & ~3; }
+
 __host__ __device__ inline int frames_of(int64_t L) {
   const int64_t Lp = L + (L % 256);  // PESQ.py:128-130: pad by L % 256 (sic)
   if (Lp < 512) return 0;
@@ -646,7 +651,20 @@ __global__ void __launch_bounds__(PT, 2)
       auto bop = [](uint32_t w, int bit, uint32_t cor) {
         return __uint_as_float(cor & (uint32_t)__builtin_amdgcn_sbfe((int)w, bit, 1));
       };
-      auto brow_of = [&](int f) { return bark + ((int64_t)it.s * F + (int64_t)g * NF + 16 * f) * NBARK; };
+      // band-major output rows (bark_ld): lane (row, kq) of frame tile f holds frames
+      // 16 f + 4 kq + i of one band -- one aligned float4 per band row
+      const int64_t fld = bark_ld(F);
+      float *__restrict__ bsig = bark + (int64_t)it.s * NBARK * fld + (int64_t)g * NF;
+      auto put4 = [&](int band, int fl, f4 v) {
+        float *o = bsig + band * fld + fl;
+        if (fl + 3 < nfr) {
+          *reinterpret_cast<f4 *>(o) = v;
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (fl + i < nfr) o[i] = v[i];
+        }
+      };
       if (wave < 3) {
         if (16 * wave < nfr) {
           const float *srow = tile + SPEC_LD * min(16 * wave + row, nfr - 1);
@@ -679,15 +697,8 @@ __global__ void __launch_bounds__(PT, 2)
               }
             }
           }
-          float *brow = brow_of(wave);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            if (16 * wave + 4 * kq + i < nfr) {
-              float *o = brow + (4 * kq + i) * NBARK;
-              o[row] = c0[i];
-              o[32 + row] = c2a[i] + c2b[i];
-            }
-          }
+          put4(row, 16 * wave + 4 * kq, c0);
+          put4(32 + row, 16 * wave + 4 * kq, c2a + c2b);
         }
       } else {
         f4 c1[3], c3[3];
@@ -718,15 +729,8 @@ __global__ void __launch_bounds__(PT, 2)
 #pragma unroll
         for (int f = 0; f < 3; ++f) {
           if (16 * f < nfr) {
-            float *brow = brow_of(f);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              if (16 * f + 4 * kq + i < nfr) {
-                float *o = brow + (4 * kq + i) * NBARK;
-                o[16 + row] = c1[f][i];
-                if (row == 0) o[48] = c3[f][i];
-              }
-            }
+            put4(16 + row, 16 * f + 4 * kq, c1[f]);
+            if (row == 0) put4(48, 16 * f + 4 * kq, c3[f]);
           }
         }
       }
@@ -756,42 +760,44 @@ __device__ __forceinline__ float pow_pos(float x, float e) {
 __device__ __forceinline__ float loud(float p, int b) {
   // loudness.py:64-65: (2T)^e ((0.5 + 0.5 P/T)^e - 1), 0 where P <= T; times Sl (folded).
   // 0.5 P/T as P * (0.5/T) (one rounding instead of a correctly rounded division: <=1 ulp)
-  const float t = kThresh[b];
-  if (!(p > t)) return 0.f;
-  return kLoud2TE[b] * (pow_pos(fmaf(p, kHalfInvThresh[b], 0.5f), kLoudExp[b]) - 1.f);
+  // branch-free (p >= 0: the pow argument is >= 0.5 either way)
+  const float v = kLoud2TE[b] * (pow_pos(fmaf(p, kHalfInvThresh[b], 0.5f), kLoudExp[b]) - 1.f);
+  return (p > kThresh[b]) ? v : 0.f;
 }
 
-// Frames are processed in chunks of BC staged in LDS by coalesced loads ([frame][49] rows are
-// contiguous per signal); lane = frame for the per-frame math, lane = band for band sums.
-constexpr int BT = 128;   // threads per workgroup
-constexpr int BC = BT;    // frames per chunk
-constexpr int BLD = 49;   // odd row stride: lane = frame reads are bank-conflict-free
+// One wave per utterance, lane = frame: each load brings one band of 64 consecutive frames
+// (band-major rows, bark_ld), straight into registers -- no LDS staging, so occupancy is set
+// by VGPRs alone (the frame's 49 clean and 49 denoised band values stay in registers per chunk).
+constexpr int BT = 64;
 
-__device__ __forceinline__ void stage_chunk(float *__restrict__ dst, const float *__restrict__ src, int nf,
-                                            int tid) {
-  const int n = nf * NBARK;
-  for (int i = tid; i < n; i += BT) dst[i] = src[i];
-}
-
-__global__ void __launch_bounds__(BT)
+__global__ void __launch_bounds__(BT) __attribute__((amdgpu_waves_per_eu(4)))
     pesq_back(const float *__restrict__ bark, const float *__restrict__ power, int64_t B, int64_t Lcap,
               const int32_t *__restrict__ lens, int Fcap, float *__restrict__ scratch, float *__restrict__ mos) {
-  __shared__ float C[BC * BLD], N[BC * BLD];
-  __shared__ float ratio[NBARK];
-  __shared__ float frs[BC + 1];
-  __shared__ double dred[4];
-  __shared__ float bsum[2][2][64];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar branches)
+  const int lane = threadIdx.x;
   const int64_t b = blockIdx.x;
   const int64_t L = row_length(lens, b, Lcap);
-  const int F = frames_of(L);  // this utterance's frames; rows are laid out with stride Fcap
+  const int F = frames_of(L);  // this utterance's frames; rows are laid out with stride bark_ld(Fcap)
   if (F < 20) {  // the reference's unfold(1, 20, 10) raises here (PESQ.py:169)
-    if (tid == 0) mos[b] = __builtin_nanf("");
+    if (lane == 0) mos[b] = __builtin_nanf("");
     return;
   }
-  const float *__restrict__ bc = bark + (b * (int64_t)Fcap) * NBARK;
-  const float *__restrict__ bn = bark + ((b + B) * (int64_t)Fcap) * NBARK;
+  const int64_t fld = bark_ld(Fcap);
+  const float *__restrict__ bc = bark + b * NBARK * fld;
+  const float *__restrict__ bn = bark + (b + B) * NBARK * fld;
+  // band rows by raw buffer loads (voffset = 4 * (k * fld + frame))
+  auto rsrc = [](const float *p, int64_t n) {
+    const uint64_t base = reinterpret_cast<uint64_t>(p);
+    // uint32_t: readfirstlane returns int, which would sign-extend into the high word
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
+    void *q = reinterpret_cast<void *>(((uint64_t)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(q, 0, (int)(n * 4), 0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t rcl = rsrc(bc, NBARK * fld), rdn = rsrc(bn, NBARK * fld);
+  const int fstride = 4 * (int)fld;  // one signal's bands span < 2^29 floats
+  auto ld = [](__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+  };
   // scratch row of this utterance: [sym | asym] per frame (stride 4 * Fcap, two slots unused)
   float *__restrict__ sym = scratch + b * (int64_t)Fcap * 4;
   float *__restrict__ asym = sym + F;
@@ -800,104 +806,129 @@ __global__ void __launch_bounds__(BT)
   const float pn = power[b + B] / (float)(L + 5120) / 1.04684f;
   const float sc = 1e7f / pc, sn = 1e7f / pn;
 
-  // ---- pass 1: silent frames (PESQ.py:146, loudness.py:48-53 x 1e2) + band means (:55-60)
-  float mc = 0.f, mn = 0.f;
-  for (int f0 = 0; f0 < F; f0 += BC) {
-    const int nf = min(BC, F - f0);
-    lds_barrier();  // LDS only: leaves the sym/asym stores in flight
-    stage_chunk(C, bc + (int64_t)f0 * NBARK, nf, tid);
-    stage_chunk(N, bn + (int64_t)f0 * NBARK, nf, tid);
-    lds_barrier();  // LDS only: leaves the sym/asym stores in flight
-    if (tid < nf) {
-      float a = 0.f;
-#pragma unroll 7
-      for (int k = 0; k < NBARK; ++k) {
-        const float c = C[tid * BLD + k] * sc;
-        a += (c > kThresh[k] * 100.f) ? c : 0.f;
-      }
-      const float sil = (a < 1e7f) ? 1.f : 0.f;
-      frs[tid] = sil;
+  // ---- pass 1: silent frames (PESQ.py:146, loudness.py:48-53 x 1e2) and per-lane partial band
+  // sums of the audible power of non-silent frames (loudness.py:55-60).  The clean sweep keeps
+  // each chunk's keep flags as a ballot (LDS), so the denoised sums follow in a second sweep
+  // without the clean accumulators live.
+  extern __shared__ unsigned long long keepm[];  // [ceil(Fcap / 64)]
+  __shared__ float ratio_s[NBARK];
+  float acc[NBARK];
+#pragma unroll
+  for (int k = 0; k < NBARK; ++k) acc[k] = 0.f;
+  for (int f0 = 0; f0 < F; f0 += BT) {
+    const int f = f0 + lane;
+    const bool valid = f < F;
+    const int fi = valid ? f : F - 1;  // clamped: every load in bounds, results masked
+    int fs = fstride;
+    asm volatile("" : "+s"(fs));  // per-chunk: keeps the 49 band offsets out of live SGPRs
+    float aud[NBARK];  // audible clean power of each band (values, not compare masks: SGPRs)
+    float a = 0.f;
+#pragma unroll
+    for (int k = 0; k < NBARK; ++k) {
+      const float c = ld(rcl, 4 * fi + k * fs, 0) * sc;
+      aud[k] = (c > kThresh[k] * 100.f) ? c : 0.f;
+      a += aud[k];
     }
-    lds_barrier();  // LDS only: leaves the sym/asym stores in flight
-    if (lane < NBARK) {
-      const float t100 = kThresh[lane] * 100.f;
-#pragma unroll 4
-      for (int f = wave; f < nf; f += 2) {
-        const float keep = (frs[f] == 0.f) ? 1.f : 0.f;  // silent frames excluded (branch-free)
-        const float c = C[f * BLD + lane] * sc;
-        const float n = N[f * BLD + lane] * sn;
-        mc += (c > t100) ? c * keep : 0.f;
-        mn += (n > t100) ? n * keep : 0.f;
+    const bool keep = valid && !(a < 1e7f);
+    const unsigned long long km = __ballot(keep);
+    if (lane == 0) keepm[f0 / BT] = km;
+#pragma unroll
+    for (int k = 0; k < NBARK; ++k) acc[k] += keep ? aud[k] : 0.f;
+  }
+  // lane-partial band sums -> totals by an LDS transpose, 16 bands per round (row = band over
+  // the 64 lanes, stride 65: conflict-free both ways); lane k < 49 ends up holding band k's total
+  __shared__ float red[16 * 65];
+  auto band_totals = [&](float v[NBARK]) {
+    float t = 0.f;
+#pragma unroll
+    for (int k0 = 0; k0 < NBARK; k0 += 16) {
+#pragma unroll
+      for (int k = k0; k < k0 + 16 && k < NBARK; ++k) red[(k - k0) * 65 + lane] = v[k];
+      __syncthreads();
+      if (lane >= k0 && lane < k0 + 16 && lane < NBARK) {
+#pragma unroll 16
+        for (int j = 0; j < 64; ++j) t += red[(lane - k0) * 65 + j];
       }
+      __syncthreads();
+    }
+    return t;
+  };
+  const float mc_tot = band_totals(acc);
+#pragma unroll
+  for (int k = 0; k < NBARK; ++k) acc[k] = 0.f;
+  for (int f0 = 0; f0 < F; f0 += BT) {
+    const int f = f0 + lane;
+    const int fi = f < F ? f : F - 1;
+    int fs = fstride;
+    asm volatile("" : "+s"(fs));
+    const bool keep = (keepm[f0 / BT] >> lane) & 1ull;
+#pragma unroll
+    for (int k = 0; k < NBARK; ++k) {
+      const float n = ld(rdn, 4 * fi + k * fs, 0) * sn;
+      acc[k] += (keep && n > kThresh[k] * 100.f) ? n : 0.f;
     }
   }
-  bsum[wave][0][lane] = mc;
-  bsum[wave][1][lane] = mn;
-  lds_barrier();  // LDS only: leaves the sym/asym stores in flight
-  if (tid < NBARK) {
-    const float c = (bsum[0][0][tid] + bsum[1][0][tid]) / F;
-    const float n = (bsum[0][1][tid] + bsum[1][1][tid]) / F;
-    ratio[tid] = fminf(fmaxf((n + 1000.f) / (c + 1000.f), 0.01f), 100.f);  // PESQ.py:151-152
+  const float mn_tot = band_totals(acc);
+  // band power ratio (PESQ.py:151-152)
+  if (lane < NBARK) {
+    const float c = mc_tot / (float)F, n = mn_tot / (float)F;
+    ratio_s[lane] = fminf(fmaxf((n + 1000.f) / (c + 1000.f), 0.01f), 100.f);
   }
+  __syncthreads();
 
   // ---- pass 2: frame ratio (PESQ.py:157-163), loudness, disturbances (PESQ.py:186-224)
   const float sqrt_tw = sqrtf((float)kTotalWidth);
-  float fr_prev = 0.f;  // frame power ratio of the last frame of the previous chunk
-  for (int f0 = 0; f0 < F; f0 += BC) {
-    const int nf = min(BC, F - f0);
-    lds_barrier();  // LDS only: leaves the sym/asym stores in flight
-    stage_chunk(C, bc + (int64_t)f0 * NBARK, nf, tid);
-    stage_chunk(N, bn + (int64_t)f0 * NBARK, nf, tid);
-    lds_barrier();  // LDS only: leaves the sym/asym stores in flight
-    float ac = 0.f;
-    if (tid < nf) {
-      float an = 0.f;
-#pragma unroll 7
-      for (int k = 0; k < NBARK; ++k) {
-        const float c = ratio[k] * (C[tid * BLD + k] * sc);
-        const float n = N[tid * BLD + k] * sn;
-        ac += (c > kThresh[k]) ? c : 0.f;
-        an += (n > kThresh[k]) ? n : 0.f;
-      }
-      frs[tid + 1] = (ac + 5e3f) / (an + 5e3f);
+  float fr_prev = 0.f;  // frame power ratio of the previous chunk's last frame
+  for (int f0 = 0; f0 < F; f0 += BT) {
+    const int f = f0 + lane;
+    const bool valid = f < F;
+    const int fi = valid ? f : F - 1;
+    int fs = fstride;
+    asm volatile("" : "+s"(fs));
+    float ec[NBARK], ns[NBARK];
+    float ac = 0.f, an = 0.f;
+#pragma unroll
+    for (int k = 0; k < NBARK; ++k) {
+      ec[k] = ratio_s[k] * (ld(rcl, 4 * fi + k * fs, 0) * sc);
+      ns[k] = ld(rdn, 4 * fi + k * fs, 0) * sn;
+      ac += (ec[k] > kThresh[k]) ? ec[k] : 0.f;
+      an += (ns[k] > kThresh[k]) ? ns[k] : 0.f;
     }
-    if (tid == 0) frs[0] = fr_prev;
-    lds_barrier();  // LDS only: leaves the sym/asym stores in flight
-    fr_prev = frs[nf];
-    if (tid < nf) {
-      const int f = f0 + tid;
-      float r = (f >= 1) ? 0.8f * frs[tid + 1] + 0.2f * frs[tid] : frs[1];  // non-recursive (PESQ.py:161)
-      r = fminf(fmaxf(r, 3e-4f), 5.f);
-      float s2 = 0.f, as = 0.f;
-#pragma unroll 7
-      for (int k = 0; k < NBARK; ++k) {
-        const float ec = ratio[k] * (C[tid * BLD + k] * sc);
-        const float en = r * (N[tid * BLD + k] * sn);
-        const float lc = loud(ec, k), ln = loud(en, k);
-        float d = ln - lc;
-        const float dz = 0.25f * fminf(lc, ln);
-        d = copysignf(fmaxf(fabsf(d) - dz, 0.f), d);
-        if (k >= 1) {
-          const float wd = kWidthBark[k] * d;
-          s2 = fmaf(wd, wd, s2);
-          float a = pow_pos((en + 50.f) * __builtin_amdgcn_rcpf(ec + 50.f), 1.2f);  // ~1 ulp rcp
-          a = (a < 3.f) ? 0.f : fminf(a, 12.f);
-          as += fabsf(wd * a);
-        }
+    const float fr = (ac + 5e3f) / (an + 5e3f);
+    float prev = __shfl_up(fr, 1, 64);
+    if (lane == 0) prev = fr_prev;
+    fr_prev = __shfl(fr, 63, 64);
+    float r = (f >= 1) ? 0.8f * fr + 0.2f * prev : fr;  // non-recursive (PESQ.py:161)
+    r = fminf(fmaxf(r, 3e-4f), 5.f);
+    float s2 = 0.f, as = 0.f;
+#pragma unroll
+    for (int k = 0; k < NBARK; ++k) {
+      const float en = r * ns[k];
+      const float lc = loud(ec[k], k), ln = loud(en, k);
+      float d = ln - lc;
+      const float dz = 0.25f * fminf(lc, ln);
+      d = copysignf(fmaxf(fabsf(d) - dz, 0.f), d);
+      if (k >= 1) {
+        const float wd = kWidthBark[k] * d;
+        s2 = fmaf(wd, wd, s2);
+        float am = pow_pos((en + 50.f) * __builtin_amdgcn_rcpf(ec[k] + 50.f), 1.2f);  // ~1 ulp rcp
+        am = (am < 3.f) ? 0.f : fminf(am, 12.f);
+        as += fabsf(wd * am);
       }
-      const float sy = fmaxf(sqrt_tw * sqrtf(s2), 1e-20f);
-      const float ay = fmaxf(as, 1e-20f);
-      const float w = pow_pos((ac + 1e5f) / 1e7f, 0.04f);
+    }
+    const float sy = fmaxf(sqrt_tw * sqrtf(s2), 1e-20f);
+    const float ay = fmaxf(as, 1e-20f);
+    const float w = pow_pos((ac + 1e5f) / 1e7f, 0.04f);
+    if (valid) {
       sym[f] = fminf(sy / w, 45.f);
       asym[f] = fminf(ay / w, 45.f);
     }
   }
-  lds_barrier();  // LDS only: leaves the sym/asym stores in flight
-  __syncthreads();  // full barrier: pass 3 reads other threads' sym / asym stores
+  __syncthreads();  // pass 3 reads other lanes' sym / asym stores
   // ---- pass 3: L6 within 20-frame windows (hop 10), L2 across windows (PESQ.py:168-172)
   const int nw = (F - 20) / 10 + 1;
   double as_ = 0.0, aa_ = 0.0;
-  for (int w = tid; w < nw; w += BT) {
+  for (int w = lane; w < nw; w += BT) {
     double s6 = 0.0, a6 = 0.0;
     for (int i = 0; i < 20; ++i) {
       const double x = sym[10 * w + i], y = asym[10 * w + i];
@@ -912,13 +943,6 @@ __global__ void __launch_bounds__(BT)
   as_ = wave_sum_d(as_);
   aa_ = wave_sum_d(aa_);
   if (lane == 0) {
-    dred[2 * wave] = as_;
-    dred[2 * wave + 1] = aa_;
-  }
-  __syncthreads();
-  as_ = dred[0] + dred[2];
-  aa_ = dred[1] + dred[3];
-  if (tid == 0) {
     const double ds = sqrt(as_ / nw), da = sqrt(aa_ / nw);
     double m = 4.5 - 0.1 * ds - 0.0309 * da;              // PESQ.py:240
     m = 0.999 + 4.0 / (1.0 + exp(-1.3669 * m + 3.8224));  // PESQ.py:243
@@ -950,7 +974,7 @@ extern "C" size_t fsem_pesq_front_workspace_bytes(int64_t batch, int64_t length)
 extern "C" size_t fsem_pesq_workspace_bytes(int64_t batch, int64_t length) {
   const pesq::Geometry g = pesq::geometry(length);
   size_t bytes = fsem_pesq_front_workspace_bytes(batch, length);
-  bytes += align_up(sizeof(float) * (size_t)(2 * batch) * (size_t)g.F * pesq::NBARK, 256);  // bark
+  bytes += align_up(sizeof(float) * (size_t)(2 * batch) * pesq::NBARK * (size_t)pesq::bark_ld(g.F), 256);  // bark
   bytes += align_up(sizeof(float) * (size_t)(2 * batch), 256);                               // power
   bytes += fsem_pesq_back_workspace_bytes(batch, length);                                     // back
   return bytes;
@@ -1016,7 +1040,8 @@ extern "C" int fsem_pesq_back_f32(const float *bark, const float *power, int64_t
   if (g.F < 20 && !lengths) return FSEM_ESHORT;
   if (!ws || ws_bytes < fsem_pesq_back_workspace_bytes(batch, length)) return FSEM_EWORKSPACE;
   if (batch > 0x7fffffff) return FSEM_EINVAL;
-  hipLaunchKernelGGL(pesq::pesq_back, dim3((unsigned)batch), dim3(pesq::BT), 0, (hipStream_t)stream, bark,
+  const size_t keep_bytes = sizeof(unsigned long long) * (size_t)((g.F + pesq::BT - 1) / pesq::BT);
+  hipLaunchKernelGGL(pesq::pesq_back, dim3((unsigned)batch), dim3(pesq::BT), keep_bytes, (hipStream_t)stream, bark,
                      power, batch, length, lengths, g.F, static_cast<float *>(ws), mos);
   FSEM_CHECK_LAUNCH();
   return FSEM_OK;
@@ -1058,7 +1083,7 @@ int fsem::pesq::run_wb(const float *ref, const float *deg, int64_t batch, int64_
   char *p = static_cast<char *>(ws);
   const size_t front = fsem_pesq_front_workspace_bytes(batch, length);
   float *bark = reinterpret_cast<float *>(p + front);
-  p += front + align_up(sizeof(float) * (size_t)(2 * batch) * (size_t)g.F * pesq::NBARK, 256);
+  p += front + align_up(sizeof(float) * (size_t)(2 * batch) * pesq::NBARK * (size_t)pesq::bark_ld(g.F), 256);
   float *power = reinterpret_cast<float *>(p);
   p += align_up(sizeof(float) * (size_t)(2 * batch), 256);
   int rc = pesq::launch_front(ref, deg, batch, length, ld, lengths, bark, power, ws, front, y10, y_ld, vad, v_ld,

@@ -47,7 +47,7 @@ def test_pesq_front_bark_matches_reference(dev, name):
     n = torch.nn.functional.pad(n, (0, (-L) % 4)).contiguous()
     ld = c.shape[1]
     F = lib.fsem_pesq_frames(L)
-    bark = torch.empty(2 * B, F, 49, device=dev)
+    bark = torch.empty(2 * B, 49, (F + 3) // 4 * 4, device=dev)  # band-major, rows padded to 4 frames
     power = torch.empty(2 * B, device=dev)
     ws = _native.workspace(lib.fsem_pesq_front_workspace_bytes(B, L), dev)
     _native.check(lib.fsem_pesq_front_f32(c.data_ptr(), n.data_ptr(), B, L, ld, None, bark.data_ptr(), power.data_ptr(),
@@ -55,7 +55,7 @@ def test_pesq_front_bark_matches_reference(dev, name):
     torch.cuda.synchronize()
     p = power.double().cpu().numpy() / (L + 5120) / 1.04684
     # golden bark is after equalize_ranges + level alignment: scale = 1e7 / power of the raw signal
-    scaled = bark.double().cpu().numpy() * (1e7 / p)[:, None, None]
+    scaled = bark[:, :, :F].transpose(1, 2).double().cpu().numpy() * (1e7 / p)[:, None, None]
     ref = g["bark"].astype(np.float64)
     rel = np.abs(scaled - ref).max() / np.abs(ref).max()
     print(name, "bark rel err", rel)

@@ -20,7 +20,7 @@ lib = _native.load()
 B, L = a.batch, 160000
 c, n, _ = speech_like_pairs(B, L, device="cuda")
 F = lib.fsem_pesq_frames(L)
-bark = torch.empty(2 * B, F, 49, device="cuda")
+bark = torch.empty(2 * B, 49, (F + 3) // 4 * 4, device="cuda")
 power = torch.empty(2 * B, device="cuda")
 ws = _native.workspace(lib.fsem_pesq_front_workspace_bytes(B, L), "cuda")
 h = torch.cuda.current_stream().cuda_stream
