@@ -312,19 +312,34 @@ __global__ void __launch_bounds__(256)
 
   // overlap-added blocks q = k0+1 .. kend+1:  block_q[t] = w[t] F_{i_q}[t] + w[128+t] F_{i_{q-1}}[128+t]
   const int nblk = kend - k0 + 1;
-#pragma unroll 3  // three blocks' loads in flight per wave
-  for (int j = wave; j < nblk; j += 4) {
+  // every block of the wave in flight at once (one memory latency round): blocks past nblk
+  // re-read the last block (clamped kept index) and are not stored
+  constexpr int NBW = (TF + 1 + 3) / 4;  // blocks per wave
+  float g[NBW][8];
+#pragma unroll
+  for (int u = 0; u < NBW; ++u) {
+    const int j = min(wave + 4 * u, nblk - 1);
     const int q = k0 + 1 + j;
     const int iq = kidx[q], ip = kidx[q - 1];
     const int64_t a0 = 128LL * iq, a1 = 128LL * ip + 128;
-    const float c0 = w_lo * at(rc, a0 + lane) + w_hi * at(rc, a1 + lane);
-    const float c1 = w_lo2 * at(rc, a0 + 64 + lane) + w_hi2 * at(rc, a1 + 64 + lane);
-    const float d0 = w_lo * at(rd, a0 + lane) + w_hi * at(rd, a1 + lane);
-    const float d1 = w_lo2 * at(rd, a0 + 64 + lane) + w_hi2 * at(rd, a1 + 64 + lane);
-    blk[0][j][lane] = c0;
-    blk[0][j][lane + 64] = c1;
-    blk[1][j][lane] = d0;
-    blk[1][j][lane + 64] = d1;
+    g[u][0] = at(rc, a0 + lane);
+    g[u][1] = at(rc, a1 + lane);
+    g[u][2] = at(rc, a0 + 64 + lane);
+    g[u][3] = at(rc, a1 + 64 + lane);
+    g[u][4] = at(rd, a0 + lane);
+    g[u][5] = at(rd, a1 + lane);
+    g[u][6] = at(rd, a0 + 64 + lane);
+    g[u][7] = at(rd, a1 + 64 + lane);
+  }
+#pragma unroll
+  for (int u = 0; u < NBW; ++u) {
+    const int j = wave + 4 * u;
+    if (j < nblk) {
+      blk[0][j][lane] = w_lo * g[u][0] + w_hi * g[u][1];
+      blk[0][j][lane + 64] = w_lo2 * g[u][2] + w_hi2 * g[u][3];
+      blk[1][j][lane] = w_lo * g[u][4] + w_hi * g[u][5];
+      blk[1][j][lane + 64] = w_lo2 * g[u][6] + w_hi2 * g[u][7];
+    }
   }
   lds_barrier();
 
@@ -419,9 +434,21 @@ __global__ void __launch_bounds__(SEG_T, 3)
   for (int m0 = 0; m0 < S; m0 += SEG_T) {
     lds_barrier();
     const int nf = min(W, T - m0);
-    for (int e = tid; e < NB * W; e += SEG_T) {
-      const int j = e / W, t = e - j * W;
-      XY[j][t] = (t < nf) ? (f2){xc[j * tmax + m0 + t], xd[j * tmax + m0 + t]} : (f2){0.f, 0.f};
+    // all 2 x 15 x 158 loads of the pass in flight at once (one latency round), then the stores
+    {
+      f2 va[NB], vb[NB];
+      const int t2 = tid + SEG_T;
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const float *xr = xc + j * tmax + m0, *dr = xd + j * tmax + m0;
+        va[j] = (tid < nf) ? (f2){xr[tid], dr[tid]} : (f2){0.f, 0.f};
+        vb[j] = (t2 < nf) ? (f2){xr[t2], dr[t2]} : (f2){0.f, 0.f};
+      }
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        XY[j][tid] = va[j];
+        if (t2 < W) XY[j][t2] = vb[j];
+      }
     }
     lds_barrier();
     const int m = m0 + tid;
