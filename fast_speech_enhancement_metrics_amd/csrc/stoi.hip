@@ -277,11 +277,27 @@ __global__ void __launch_bounds__(256)
   if (tid == 0) kept[b] = base;
 }
 
-__global__ void __launch_bounds__(256)
+#ifdef FSEM_STAMPS
+// Diagnostic build only (tools/tob_stamps.py): s_memtime at stoi_tob phase boundaries.
+constexpr int kTobStampBlocks = 131072;
+__device__ unsigned long long g_tob_stamps[kTobStampBlocks][4];
+#define TSTAMP(i)                                                                            \
+  do {                                                                                       \
+    const unsigned lin_ = blockIdx.y * gridDim.x + blockIdx.x;                               \
+    if (threadIdx.x == 0 && lin_ < kTobStampBlocks) g_tob_stamps[lin_][i] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define TSTAMP(i) \
+  do {            \
+  } while (0)
+#endif
+
+constexpr int TOB_WAVES = 4;  // 256-thread workgroups (8 waves x 66 KB measured no faster)
+__global__ void __launch_bounds__(64 * TOB_WAVES)
     stoi_tob(const float *__restrict__ y10, int64_t y_ld, int64_t B, Rows rows, const int *__restrict__ idx,
              const int *__restrict__ kept, int nv_ld, float *__restrict__ tob, int64_t tmax) {
   __shared__ __attribute__((aligned(16))) float blk[2][TF + 1][128];
-  __shared__ __attribute__((aligned(16))) float xbuf[4 * 2 * kFftBuf];
+  __shared__ __attribute__((aligned(16))) float xbuf[TOB_WAVES * 2 * kFftBuf];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: kept indices by scalar loads
   const int64_t b = blockIdx.y;
@@ -290,6 +306,7 @@ __global__ void __launch_bounds__(256)
   const int64_t L10 = rows.l10(b);
   const int k0 = blockIdx.x * TF;
   if (k0 >= T) return;
+  TSTAMP(0);
   const int kend = min(k0 + TF, T);
   const int *kidx = idx + b * nv_ld;
   const float *__restrict__ yc = y10 + (b * 2) * y_ld;
@@ -314,11 +331,11 @@ __global__ void __launch_bounds__(256)
   const int nblk = kend - k0 + 1;
   // every block of the wave in flight at once (one memory latency round): blocks past nblk
   // re-read the last block (clamped kept index) and are not stored
-  constexpr int NBW = (TF + 1 + 3) / 4;  // blocks per wave
+  constexpr int NBW = (TF + 1 + TOB_WAVES - 1) / TOB_WAVES;  // blocks per wave
   float g[NBW][8];
 #pragma unroll
   for (int u = 0; u < NBW; ++u) {
-    const int j = min(wave + 4 * u, nblk - 1);
+    const int j = min(wave + TOB_WAVES * u, nblk - 1);
     const int q = k0 + 1 + j;
     const int iq = kidx[q], ip = kidx[q - 1];
     const int64_t a0 = 128LL * iq, a1 = 128LL * ip + 128;
@@ -333,7 +350,7 @@ __global__ void __launch_bounds__(256)
   }
 #pragma unroll
   for (int u = 0; u < NBW; ++u) {
-    const int j = wave + 4 * u;
+    const int j = wave + TOB_WAVES * u;
     if (j < nblk) {
       blk[0][j][lane] = w_lo * g[u][0] + w_hi * g[u][1];
       blk[0][j][lane + 64] = w_lo2 * g[u][2] + w_hi2 * g[u][3];
@@ -342,6 +359,7 @@ __global__ void __launch_bounds__(256)
     }
   }
   lds_barrier();
+  TSTAMP(1);
 
   cf tw1[8], tw2[8];
   fft512_twiddles(lane, tw1, tw2);
@@ -353,7 +371,7 @@ __global__ void __launch_bounds__(256)
   const int pc_lo = kObmPiece[lane][2], pc_hi = kObmPiece[lane][3];
   const int pc_end = kObmPiece[lane][4];
   const bool pc_head = kObmPiece[lane][5] != 0;
-  for (int k = k0 + wave; k < kend; k += 4) {
+  for (int k = k0 + wave; k < kend; k += TOB_WAVES) {
     const int j = k - k0;  // frame k = [block_{k+1}, block_{k+2}] * w
     cf v[8];
 #pragma unroll
@@ -398,6 +416,7 @@ __global__ void __launch_bounds__(256)
     }
     wave_lds_fence();
   }
+  TSTAMP(2);
 }
 
 // One lane per 30-frame segment m: x[j][t] = X[j][m + t], y likewise (STOI.py:121-198).
@@ -608,7 +627,7 @@ inline int run_tail(int64_t B, const Geometry &g, const Rows &rows, const float 
                     int *kept, float *tob, int64_t tmax, float *stoi_out, float *estoi_out, hipStream_t st) {
   hipLaunchKernelGGL(stoi_select, dim3((unsigned)B), dim3(256), 0, st, vad, g.v_ld, g.nv_ld, rows, idx, kept);
   FSEM_CHECK_LAUNCH();
-  hipLaunchKernelGGL(stoi_tob, dim3((unsigned)((g.tmax + TF - 1) / TF), (unsigned)B), dim3(256), 0, st, y10,
+  hipLaunchKernelGGL(stoi_tob, dim3((unsigned)((g.tmax + TF - 1) / TF), (unsigned)B), dim3(64 * TOB_WAVES), 0, st, y10,
                      g.y_ld, B, rows, idx, kept, g.nv_ld, tob, tmax);
   FSEM_CHECK_LAUNCH();
   if (stoi_out) {
@@ -725,6 +744,15 @@ extern "C" int fsem_pesq_stoi_f32(const float *ref, const float *deg, int64_t ba
   const int rj = stream_wait(st, side);
   return rc != FSEM_OK ? rc : rj;
 }
+
+#ifdef FSEM_STAMPS
+// diagnostic build only (not part of include/fsem.h)
+extern "C" int fsem_debug_read_tob_stamps(void *dst, size_t bytes) {
+  if (hipDeviceSynchronize() != hipSuccess) return FSEM_ELAUNCH;
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(stoi::g_tob_stamps), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess
+             ? FSEM_OK : FSEM_ELAUNCH;
+}
+#endif
 
 extern "C" const char *fsem_strerror(int code) {
   switch (code) {
