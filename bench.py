@@ -128,10 +128,44 @@ def kernel_roofline(clean, noisy, reps, joint):
     ms = start.elapsed_time(end) / reps
     algo_bytes = 2 * B * L * 4  # both signals read once (2*L*4 B per pair)
     achieved = algo_bytes / (ms * 1e-3) / 1e9
-    traffic, source = pmc_traffic("pesq_front<true, false>" if joint else "pesq_front<false, false>", B, L)
-    return {"kernel": "pesq_front<joint>" if joint else "pesq_front", "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "traffic_source": source, "ms_per_launch": round(ms, 4), "algorithmic_bytes_per_launch": algo_bytes}
+    name = "pesq_front<true, false>" if joint else "pesq_front<false, false>"
+    traffic, source = pmc_traffic(name, B, L)
+    out = {"kernel": "pesq_front<joint>" if joint else "pesq_front", "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+           "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+           "traffic_source": source, "ms_per_launch": round(ms, 4), "algorithmic_bytes_per_launch": algo_bytes}
+    valu = pmc_counter(name, "SQ_INSTS_VALU", B, L)
+    if valu:
+        # the kernel is latency bound (2 waves per SIMD by its 256 VGPRs and 80 KB of LDS per
+        # workgroup), neither HBM nor VALU bound: its vector-ALU share = SQ_INSTS_VALU x 2
+        # cycles (a wave64 instruction on a SIMD-32, MI355X_MICROARCH.md) over the SIMDs x the
+        # measured launch time at the 2.4 GHz peak engine clock
+        n, src = valu
+        sims = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
+        out["valu_issue"] = {"instructions_per_launch": n, "frac": round(n * 2 / (sims * 2.4e9 * ms * 1e-3), 4),
+                             "source": src}
+    return out
+
+
+def pmc_counter(kernel: str, counter: str, B: int, L: int):
+    """(value per launch, source) of one counter of `kernel` from the newest committed PMC summary."""
+    import glob
+    import re
+    if (B, L) != (4096, 160000):
+        return None
+
+    def natural(path):
+        return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", path)]
+
+    best = None
+    for f in sorted(glob.glob(os.path.join(HERE, "profiles", "*", "pmc_summary.json")), key=natural):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        key = next((k for k in d if k.endswith(kernel)), None)
+        if key and counter in d[key]:
+            best = (int(d[key][counter]), os.path.relpath(f, HERE))
+    return best
 
 
 def pmc_traffic(kernel: str, B: int, L: int):
