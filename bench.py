@@ -96,7 +96,7 @@ def kernel_roofline(clean, noisy, reps, joint):
     B, L = clean.shape
     F = lib.fsem_pesq_frames(L)
     dev = clean.device
-    bark = torch.empty(2 * B, 49, (F + 3) // 4 * 4, device=dev)  # band-major rows (include/fsem.h)
+    bark = torch.empty(2 * B, 49, (F + 31) // 32 * 32, device=dev)  # band-major rows (include/fsem.h)
     power = torch.empty(2 * B, device=dev)
     ws = _native.workspace(lib.fsem_pesq_front_workspace_bytes(B, L), dev)
     stream = torch.cuda.current_stream(dev)

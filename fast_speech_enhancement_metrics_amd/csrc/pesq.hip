@@ -78,9 +78,11 @@ static_assert(SPEC_LD * (NF - 1) + 256 <= TILE, "parked spectra stay in the tile
 static_assert(TILE % (4 * PT) == 0, "prefetch split");
 
 // Bark bands are stored band-major per signal: bark[(s * NBARK + k) * bark_ld(F) + f], rows
-// padded to a multiple of 4 frames (aligned float4 stores from the MFMA tiles; the back end
-// reads one band of 64 consecutive frames per load, lane = frame).
-__host__ __device__ inline int64_t bark_ld(int F) { return (F + 3) & ~3; }
+// padded to a multiple of 32 frames: every row starts on a 128-byte line, so the back end's
+// loads of one band over 64 consecutive frames (lane = frame) touch exactly two lines (a
+// 4-frame padding left them straddling three: 1.25x the HBM reads), and the MFMA tiles' float4
+// stores stay aligned.
+__host__ __device__ inline int64_t bark_ld(int F) { return (F + 31) & ~31; }
 
 __host__ __device__ inline int frames_of(int64_t L) {
   const int64_t Lp = L + (L % 256);  // PESQ.py:128-130: pad by L % 256 (sic)

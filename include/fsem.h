@@ -78,7 +78,7 @@ int fsem_pesq_wb_f32(const float *ref, const float *deg, int64_t batch, int64_t 
  *        (bark.py:203-204), BEFORE the level scale:
  *          bark  [2*batch, 49, Fld] float32, band-major (signal s, band k, frame f at
  *                (s*49 + k)*Fld + f; signals 0..B-1 ref, B..2B-1 deg), unscaled,
- *                F = fsem_pesq_frames(length), Fld = F rounded up to a multiple of 4
+ *                F = fsem_pesq_frames(length), Fld = F rounded up to a multiple of 32
  *                (frames F..Fld-1 unused); a shorter row fills its first
  *                fsem_pesq_frames(lengths[b]) frames
  *          power [2*batch] float32 = sum_t filtered^2 (not yet / (L+5120) / 1.04684)

@@ -47,7 +47,7 @@ def test_pesq_front_bark_matches_reference(dev, name):
     n = torch.nn.functional.pad(n, (0, (-L) % 4)).contiguous()
     ld = c.shape[1]
     F = lib.fsem_pesq_frames(L)
-    bark = torch.empty(2 * B, 49, (F + 3) // 4 * 4, device=dev)  # band-major, rows padded to 4 frames
+    bark = torch.empty(2 * B, 49, (F + 31) // 32 * 32, device=dev)  # band-major, rows padded to 32 frames
     power = torch.empty(2 * B, device=dev)
     ws = _native.workspace(lib.fsem_pesq_front_workspace_bytes(B, L), dev)
     _native.check(lib.fsem_pesq_front_f32(c.data_ptr(), n.data_ptr(), B, L, ld, None, bark.data_ptr(), power.data_ptr(),

@@ -244,7 +244,7 @@ def test_gpu_front_y10_resampler_and_front_unchanged():
     vad = torch.full((B, v_ld, 2), float("nan"), device=dev)
     outs = []
     for joint in (False, True):
-        bark = torch.full((2 * B, 49, (F + 3) // 4 * 4), -1.0, device=dev)
+        bark = torch.full((2 * B, 49, (F + 31) // 32 * 32), -1.0, device=dev)
         power = torch.empty(2 * B, device=dev)
         y10 = torch.full((2 * B, y_ld), float("nan"), device=dev)
         ws = _native.workspace(lib.fsem_pesq_front_workspace_bytes(B, L), dev)

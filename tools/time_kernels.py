@@ -20,7 +20,7 @@ lib = _native.load()
 B, L = a.batch, 160000
 c, n, _ = speech_like_pairs(B, L, device="cuda")
 F = lib.fsem_pesq_frames(L)
-bark = torch.empty(2 * B, 49, (F + 3) // 4 * 4, device="cuda")
+bark = torch.empty(2 * B, 49, (F + 31) // 32 * 32, device="cuda")
 power = torch.empty(2 * B, device="cuda")
 ws = _native.workspace(lib.fsem_pesq_front_workspace_bytes(B, L), "cuda")
 h = torch.cuda.current_stream().cuda_stream
@@ -51,4 +51,17 @@ t_front = timeit(front)
 t_pesq = timeit(lambda: p.scores(c, n))
 t_stoi = timeit(lambda: st.scores(c, n, 16000))
 mos = p.scores(c, n)[:4].tolist()
-print(f"{os.path.basename(_native.LIB_PATH)}: pesq_front {t_front:.3f} ms  PESQ {t_pesq:.3f} ms  STOI {t_stoi:.3f} ms  joint {t_joint:.3f} ms  mos[:4] {mos}")
+# the back end alone, on the front's outputs
+front()
+mos_b = torch.empty(B, device="cuda")
+wsb = _native.workspace(lib.fsem_pesq_back_workspace_bytes(B, L), "cuda")
+
+
+def back():
+    _native.check(lib.fsem_pesq_back_f32(bark.data_ptr(), power.data_ptr(), B, L, None, mos_b.data_ptr(),
+                                         wsb.data_ptr(), wsb.numel(), h), "back")
+
+
+t_back = timeit(back)
+print(f"{os.path.basename(_native.LIB_PATH)}: pesq_front {t_front:.3f} ms  pesq_back {t_back:.3f} ms  PESQ {t_pesq:.3f} ms  "
+      f"STOI {t_stoi:.3f} ms  joint {t_joint:.3f} ms  mos[:4] {mos}")
