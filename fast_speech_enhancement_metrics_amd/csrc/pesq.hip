@@ -512,6 +512,10 @@ __global__ void __launch_bounds__(PT, 2)
     // double-buffered (read one half, write the other): one barrier per level
     float *sbuf = xbuf;
     float *dbuf = xbuf + PT * SCAN_LD;
+    // joint entry: the scan states of wave w+1 land in wave w's resampler staging slice
+    // (xbuf[960 w, 960 w + 960) vs [832 (w+1), 832 (w+2))), so every wave must be done with its
+    // staged outputs first
+    if (JOINT) lds_barrier();
 #pragma unroll
     for (int i = 0; i < NS; ++i) sbuf[tid * SCAN_LD + i] = e[i];
     lds_barrier();
