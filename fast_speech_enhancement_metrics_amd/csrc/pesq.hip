@@ -66,14 +66,21 @@ constexpr int OWN = NF * 256;     // samples of band-pass power owned per segmen
 constexpr int NBARK = 49;
 constexpr int NS = 12;            // scan states: 10 band-pass (5 sections) + 2 pre-emphasis
 constexpr int SCAN_LD = 13;       // floats per lane in the scan buffer (odd: conflict-free)
-// exchange buffer: 4 waves x 576 complex for the FFTs, or the two halves of the double-buffered
-// chunk scan (2 x 256 x 13 floats); with the tile, 79 968 B per workgroup: 2 fit a CU
-constexpr int XBUF = 2 * PT * 13 > 4 * 2 * kFftBuf ? 2 * PT * 13 : 4 * 2 * kFftBuf;
+// exchange buffer: 4 waves x 512 complex for the FFTs, the resampler's per-wave staging slices
+// (4 x 960 floats, joint entry), or the two buffers of the double-buffered chunk scan.  Scan
+// buffer A keeps wave w's states inside wave w's own staging slice (960 w + 13 lane: no wave
+// writes into a slice another wave may still be reading, and no barrier is needed between the
+// resampler and the scan); buffer B (first written after a barrier) is packed after A's last
+// state.  With the tile, 81 568 B per workgroup: 2 fit a CU.
+constexpr int SCAN_A_WAVE = 960;                               // = the resampler's RS_STAGE
+constexpr int SCAN_B0 = 3 * SCAN_A_WAVE + 64 * 13;             // 3712: just past buffer A
+constexpr int XBUF = SCAN_B0 + PT * 13;                        // 7040 floats
+static_assert(XBUF >= 4 * 2 * kFftBuf, "FFT exchange areas fit");
 constexpr int SPEC_LD = 258;      // parked spectrum row stride: = 2 mod 32, MFMA A reads conflict-free
 constexpr int NBP = 10;           // band-pass states
 constexpr int PF = TILE / 4 / PT; // float4 per thread per tile (prefetch registers)
 static_assert(WARM + 256 * (NF + 1) == TILE, "tile geometry");
-static_assert(2 * PT * SCAN_LD <= XBUF, "double-buffered scan fits the exchange buffer");
+static_assert(SCAN_LD == 13 && 64 * SCAN_LD <= SCAN_A_WAVE, "scan buffer A: a wave's states within its staging slice");
 static_assert(SPEC_LD * (NF - 1) + 256 <= TILE, "parked spectra stay in the tile");
 static_assert(TILE % (4 * PT) == 0, "prefetch split");
 
@@ -281,7 +288,7 @@ static_assert((WARM - 12) % 4 == 0, "16-byte aligned tap reads");
 constexpr int RS_KS = 11;                  // K-steps (44 taps)
 constexpr int RS_TILES = 4;                // 16-super-group MFMA tiles per wave step
 constexpr int RS_STAGE = RS_TILES * 16 * 15;  // outputs per wave step (960)
-static_assert(4 * RS_STAGE <= XBUF, "resampler staging fits the exchange buffer");
+static_assert(4 * RS_STAGE <= XBUF && RS_STAGE == SCAN_A_WAVE, "resampler staging slices = scan buffer A slices");
 static_assert(OWN10 % RS_STAGE == 0 && OWN10 / RS_STAGE == 8, "two wave steps per wave and segment");
 // the last segment owns up to (TILE - WARM) * 5 / 8 outputs; the taps of its last super-group
 // (x 0 coefficients included: a NaN there would poison the row) stay in the zeroed pad.  Rows
@@ -509,21 +516,20 @@ __global__ void __launch_bounds__(PT, 2)
       iir_pass1<false>(my4, t_lane, L, e);
     STAMP(2);
     // ---------------------------------------------------------------- chunk scan (4 levels)
-    // double-buffered (read one half, write the other): one barrier per level
-    float *sbuf = xbuf;
-    float *dbuf = xbuf + PT * SCAN_LD;
-    // joint entry: the scan states of wave w+1 land in wave w's resampler staging slice
-    // (xbuf[960 w, 960 w + 960) vs [832 (w+1), 832 (w+2))), so every wave must be done with its
-    // staged outputs first
-    if (JOINT) lds_barrier();
+    // double-buffered (read one buffer, write the other): one barrier per level.  Buffer A at
+    // 960 (tid / 64) + 13 (tid % 64) (inside the wave's own resampler staging slice), buffer B
+    // at SCAN_B0 + 13 tid; levels 0..3 read A, B, A, B.
+    auto scan_at = [&](bool in_b, int t) {
+      return in_b ? xbuf + SCAN_B0 + t * SCAN_LD : xbuf + SCAN_A_WAVE * (t >> 6) + (t & 63) * SCAN_LD;
+    };
 #pragma unroll
-    for (int i = 0; i < NS; ++i) sbuf[tid * SCAN_LD + i] = e[i];
+    for (int i = 0; i < NS; ++i) scan_at(false, tid)[i] = e[i];
     lds_barrier();
 #pragma unroll
     for (int lv = 0; lv < 4; ++lv) {
       const int d = 1 << lv;
       float q[NS];
-      const float *src = sbuf + max(tid - d, 0) * SCAN_LD;  // one base + immediate offsets
+      const float *src = scan_at(lv & 1, max(tid - d, 0));  // one base + immediate offsets
       const float keep = (tid >= d) ? 1.f : 0.f;
 #pragma unroll
       for (int i = 0; i < NS; ++i) q[i] = src[i] * keep;
@@ -541,17 +547,15 @@ __global__ void __launch_bounds__(PT, 2)
         e[NBP] = p0;
         e[NBP + 1] = p1;
       }
+      float *dst = scan_at(!(lv & 1), tid);
 #pragma unroll
-      for (int i = 0; i < NS; ++i) dbuf[tid * SCAN_LD + i] = e[i];
+      for (int i = 0; i < NS; ++i) dst[i] = e[i];
       lds_barrier();
-      float *t = sbuf;
-      sbuf = dbuf;
-      dbuf = t;
     }
-    // start state of chunk j = inclusive prefix of chunk j-1
+    // start state of chunk j = inclusive prefix of chunk j-1 (level 3 wrote buffer A)
     float z[NS];
     {
-      const float *src = sbuf + max(tid - 1, 0) * SCAN_LD;
+      const float *src = scan_at(false, max(tid - 1, 0));
       const float keep = (tid >= 1) ? 1.f : 0.f;
 #pragma unroll
       for (int i = 0; i < NS; ++i) z[i] = src[i] * keep;
