@@ -17,6 +17,12 @@ namespace pesq {
 int launch_front(const float *ref, const float *deg, int64_t batch, int64_t length, int64_t ld,
                  const int32_t *lengths, float *bark, float *power, void *ws, size_t ws_bytes, float *y10,
                  int64_t y_ld, float2 *vad, int64_t v_ld, hipStream_t st);
+// the two halves of run_wb on one workspace (fsem_pesq_workspace_bytes): the front end (as
+// launch_front) and, once it is complete on back_st, the back end writing mos
+int run_wb_front(const float *ref, const float *deg, int64_t batch, int64_t length, int64_t ld,
+                 const int32_t *lengths, void *ws, size_t ws_bytes, float *y10, int64_t y_ld, float2 *vad,
+                 int64_t v_ld, hipStream_t st);
+int run_wb_back(int64_t batch, int64_t length, const int32_t *lengths, float *mos, void *ws, hipStream_t back_st);
 // whole PESQ-wb (front + back), optionally emitting y10 as above; the back end runs on back_st
 // after the front end on st (back_st == st: one stream)
 int run_wb(const float *ref, const float *deg, int64_t batch, int64_t length, int64_t ld, const int32_t *lengths,

@@ -1083,26 +1083,54 @@ int fsem::stream_wait(hipStream_t waiter, hipStream_t producer) {
   return ok ? FSEM_OK : FSEM_ELAUNCH;
 }
 
-int fsem::pesq::run_wb(const float *ref, const float *deg, int64_t batch, int64_t length, int64_t ld,
-                       const int32_t *lengths, float *mos, void *ws, size_t ws_bytes, float *y10, int64_t y_ld,
-                       float2 *vad, int64_t v_ld, hipStream_t stream, hipStream_t back_st) {
-  if (!ref || !deg || !mos || batch <= 0 || length <= 0 || ld < length) return FSEM_EINVAL;
+// Workspace of the whole-metric entry: [front partials | bark | power | back scratch].
+struct WbWs {
+  size_t front;
+  float *bark, *power;
+  char *back;
+};
+static WbWs carve_wb(void *ws, int64_t batch, int64_t length) {
+  const pesq::Geometry g = pesq::geometry(length);
+  WbWs w;
+  char *p = static_cast<char *>(ws);
+  w.front = fsem_pesq_front_workspace_bytes(batch, length);
+  w.bark = reinterpret_cast<float *>(p + w.front);
+  p += w.front + align_up(sizeof(float) * (size_t)(2 * batch) * pesq::NBARK * (size_t)pesq::bark_ld(g.F), 256);
+  w.power = reinterpret_cast<float *>(p);
+  p += align_up(sizeof(float) * (size_t)(2 * batch), 256);
+  w.back = p;
+  return w;
+}
+
+int fsem::pesq::run_wb_front(const float *ref, const float *deg, int64_t batch, int64_t length, int64_t ld,
+                             const int32_t *lengths, void *ws, size_t ws_bytes, float *y10, int64_t y_ld,
+                             float2 *vad, int64_t v_ld, hipStream_t stream) {
+  if (!ref || !deg || batch <= 0 || length <= 0 || ld < length) return FSEM_EINVAL;
   const pesq::Geometry g = pesq::geometry(length);
   if (g.F < 20 && !lengths) return FSEM_ESHORT;
   if (!ws || ws_bytes < fsem_pesq_workspace_bytes(batch, length)) return FSEM_EWORKSPACE;
-  char *p = static_cast<char *>(ws);
-  const size_t front = fsem_pesq_front_workspace_bytes(batch, length);
-  float *bark = reinterpret_cast<float *>(p + front);
-  p += front + align_up(sizeof(float) * (size_t)(2 * batch) * pesq::NBARK * (size_t)pesq::bark_ld(g.F), 256);
-  float *power = reinterpret_cast<float *>(p);
-  p += align_up(sizeof(float) * (size_t)(2 * batch), 256);
-  int rc = pesq::launch_front(ref, deg, batch, length, ld, lengths, bark, power, ws, front, y10, y_ld, vad, v_ld,
-                              stream);
+  const WbWs w = carve_wb(ws, batch, length);
+  return pesq::launch_front(ref, deg, batch, length, ld, lengths, w.bark, w.power, ws, w.front, y10, y_ld, vad,
+                            v_ld, stream);
+}
+
+int fsem::pesq::run_wb_back(int64_t batch, int64_t length, const int32_t *lengths, float *mos, void *ws,
+                            hipStream_t back_st) {
+  if (!mos) return FSEM_EINVAL;
+  const WbWs w = carve_wb(ws, batch, length);
+  return fsem_pesq_back_f32(w.bark, w.power, batch, length, lengths, mos, w.back,
+                            fsem_pesq_back_workspace_bytes(batch, length), back_st);
+}
+
+int fsem::pesq::run_wb(const float *ref, const float *deg, int64_t batch, int64_t length, int64_t ld,
+                       const int32_t *lengths, float *mos, void *ws, size_t ws_bytes, float *y10, int64_t y_ld,
+                       float2 *vad, int64_t v_ld, hipStream_t stream, hipStream_t back_st) {
+  if (!mos) return FSEM_EINVAL;
+  int rc = run_wb_front(ref, deg, batch, length, ld, lengths, ws, ws_bytes, y10, y_ld, vad, v_ld, stream);
   if (rc != FSEM_OK) return rc;
   rc = stream_wait(back_st, stream);
   if (rc != FSEM_OK) return rc;
-  return fsem_pesq_back_f32(bark, power, batch, length, lengths, mos, p,
-                            fsem_pesq_back_workspace_bytes(batch, length), back_st);
+  return run_wb_back(batch, length, lengths, mos, ws, back_st);
 }
 
 extern "C" int fsem_pesq_wb_f32(const float *ref, const float *deg, int64_t batch, int64_t length,

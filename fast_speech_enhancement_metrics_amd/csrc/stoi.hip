@@ -638,6 +638,13 @@ inline int run_tail(int64_t B, const Geometry &g, const Rows &rows, const float 
   return FSEM_OK;
 }
 
+inline int run_seg(int64_t B, const float *tob, int64_t tmax, const int *kept, float *stoi_out, float *estoi_out,
+                   hipStream_t st) {
+  hipLaunchKernelGGL(stoi_seg, dim3((unsigned)B), dim3(SEG_T), 0, st, tob, B, tmax, kept, stoi_out, estoi_out);
+  FSEM_CHECK_LAUNCH();
+  return FSEM_OK;
+}
+
 inline int run(const float *ref, const float *deg, int64_t B, int64_t length, int64_t ld,
                const int32_t *lengths, int32_t sr, float *stoi_out, float *estoi_out, int32_t *kept_out,
                float *tob_out, int64_t tob_ld, void *ws, size_t ws_size, hipStream_t st) {
@@ -734,13 +741,19 @@ extern "C" int fsem_pesq_stoi_f32(const float *ref, const float *deg, int64_t ba
   const stoi::Rows rows{lengths, length, rk.orig, rk.nw};
   hipStream_t st = (hipStream_t)stream;
   // PESQ-wb with the 10 kHz rows emitted from the same input tiles.  The PESQ back end (one
-  // workgroup per pair, low occupancy) runs on a side stream concurrently with the STOI tail;
+  // wave per pair) runs on a side stream concurrently with the STOI segment kernel (VALU bound,
+  // where the back end's latency-bound waves fit in better than beside the LDS-bound stoi_tob);
   // both only read what the front end wrote, and the caller's stream joins the side stream.
   const hipStream_t side = side_stream(st);
-  rc = pesq::run_wb(ref, deg, batch, length, ld, lengths, mos, ws, pesq_bytes, w.y10, g.y_ld, w.vad, g.v_ld, st,
-                    side);
+  rc = pesq::run_wb_front(ref, deg, batch, length, ld, lengths, ws, pesq_bytes, w.y10, g.y_ld, w.vad, g.v_ld, st);
   if (rc != FSEM_OK) return rc;
-  rc = stoi::run_tail(batch, g, rows, w.y10, w.vad, w.idx, w.kept, w.tob, g.tmax, stoi_out, estoi_out, st);
+  rc = stoi::run_tail(batch, g, rows, w.y10, w.vad, w.idx, w.kept, w.tob, g.tmax, nullptr, nullptr, st);
+  if (rc != FSEM_OK) return rc;
+  rc = stream_wait(side, st);
+  if (rc != FSEM_OK) return rc;
+  rc = pesq::run_wb_back(batch, length, lengths, mos, ws, side);
+  if (rc != FSEM_OK) return rc;
+  rc = stoi::run_seg(batch, w.tob, g.tmax, w.kept, stoi_out, estoi_out, st);
   const int rj = stream_wait(st, side);
   return rc != FSEM_OK ? rc : rj;
 }
