@@ -351,13 +351,14 @@ __global__ void __launch_bounds__(64 * TOB_WAVES)
 #pragma unroll
   for (int u = 0; u < NBW; ++u) {
     const int j = wave + TOB_WAVES * u;
-    if (j < nblk) {
-      blk[0][j][lane] = w_lo * g[u][0] + w_hi * g[u][1];
-      blk[0][j][lane + 64] = w_lo2 * g[u][2] + w_hi2 * g[u][3];
-      blk[1][j][lane] = w_lo * g[u][4] + w_hi * g[u][5];
-      blk[1][j][lane + 64] = w_lo2 * g[u][6] + w_hi2 * g[u][7];
+    if (j < nblk) {  // uniform: lane-ordered stores without address VGPRs
+      lds_store_lanes(&blk[0][j][0], w_lo * g[u][0] + w_hi * g[u][1]);
+      lds_store_lanes(&blk[0][j][64], w_lo2 * g[u][2] + w_hi2 * g[u][3]);
+      lds_store_lanes(&blk[1][j][0], w_lo * g[u][4] + w_hi * g[u][5]);
+      lds_store_lanes(&blk[1][j][64], w_lo2 * g[u][6] + w_hi2 * g[u][7]);
     }
   }
+  lds_stores_done();  // other waves read these blocks
   lds_barrier();
   TSTAMP(1);
 
@@ -397,8 +398,8 @@ __global__ void __launch_bounds__(64 * TOB_WAVES)
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      pbuf[lane + 64 * r] = pc[r];
-      pbuf[256 + lane + 64 * r] = pd[r];
+      lds_store_lanes(pbuf + 64 * r, pc[r]);
+      lds_store_lanes(pbuf + 256 + 64 * r, pd[r]);
     }
     wave_lds_fence();
     {
