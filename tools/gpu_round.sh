@@ -8,7 +8,7 @@ OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 timeout -k 10 600 python -m pytest tests -m gpu -x -q -s > $OUT/gpu_tests.log 2>&1 || { echo "TESTS FAILED"; tail -30 $OUT/gpu_tests.log; exit 1; }
 tail -3 $OUT/gpu_tests.log
-timeout -k 10 600 python bench.py --steps 10 --warmup 2 > $OUT/bench.json 2> $OUT/bench.err || { echo "BENCH FAILED"; tail -20 $OUT/bench.err; exit 1; }
+timeout -k 10 600 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo "BENCH FAILED"; tail -20 $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python $R/tools/one_step.py --reps 3 --joint > $OUT/trace.log 2>&1 || { echo "TRACE FAILED"; tail -20 $OUT/trace.log; exit 1; }
