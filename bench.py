@@ -39,8 +39,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=10,
+                    help="untimed steps: the engine's step time settles over ~5 steps after the first "
+                         "(workspace allocation, clocks)")
     ap.add_argument("--batch", type=int, default=4096, help="utterance pairs per GPU")
     ap.add_argument("--length", type=int, default=160000, help="samples per utterance (16 kHz)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget")
