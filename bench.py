@@ -287,7 +287,7 @@ def run_c5(args, world, rank, dev, distributed):
         out16 = torch.stack(joint.scores(c, n, lengths=l16), 1)
         c8, n8, l8 = groups[8000]
         l8to16 = resampled_lengths(l8, 8000, 16000).to(dev)
-        mos8 = p8.scores(up(c8), up(n8), lengths=l8to16)
+        mos8 = p8.scores(up(c8, l8), up(n8, l8), lengths=l8to16)  # each row resampled as the row alone
         st8, es8 = s8.scores(c8, n8, 8000, lengths=l8)
         out8 = torch.stack([mos8, st8, es8], 1)
         res = torch.cat([out8, out16])

@@ -37,6 +37,7 @@ SIGNATURES = {
     "fsem_version": (ctypes.c_int, []),
     "fsem_resample_length": (_c_i64, [_c_i64, _c_i32, _c_i32]),
     "fsem_resample_f32": (ctypes.c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _c_i64, _c_i32, _c_i32, _vp]),
+    "fsem_resample_rows_f32": (ctypes.c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_i64, _c_i32, _c_i32, _vp]),
     "fsem_pesq_workspace_bytes": (_c_sz, [_c_i64, _c_i64]),
     "fsem_pesq_frames": (ctypes.c_int, [_c_i64]),
     "fsem_pesq_wb_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _c_sz, _vp]),

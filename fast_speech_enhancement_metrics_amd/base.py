@@ -30,19 +30,22 @@ class BaseMetric(ABC):
                 raise RuntimeError("use_gpu=True but no HIP device is visible")
             _native.load()
 
-    def prepare_audio(self, audio: torch.Tensor) -> torch.Tensor:
+    def prepare_audio(self, audio: torch.Tensor, lengths: torch.Tensor | None = None) -> torch.Tensor:
+        """The reference's prepare_audio (base.py:16-21); with ``lengths`` each row is resampled as
+        its unpadded self (Resample.forward)."""
         audio = torch.atleast_2d(audio)
         audio = audio.to(self.device)
         if self.sample_rate != self.EXPECTED_SAMPLING_RATE:
-            audio = self.resampler(audio)
+            audio = self.resampler(audio, lengths)
         return audio
 
-    def prepare_inputs(self, clean_speech: torch.Tensor | None, denoised_speech: torch.Tensor):
+    def prepare_inputs(self, clean_speech: torch.Tensor | None, denoised_speech: torch.Tensor,
+                       lengths: torch.Tensor | None = None):
         if clean_speech is not None and clean_speech.shape != denoised_speech.shape:
             raise Exception("`clean_speech` and `denoised_speech` should have the same shape.")
         if clean_speech is not None:
-            clean_speech = self.prepare_audio(clean_speech)
-        denoised_speech = self.prepare_audio(denoised_speech)
+            clean_speech = self.prepare_audio(clean_speech, lengths)
+        denoised_speech = self.prepare_audio(denoised_speech, lengths)
         return clean_speech, denoised_speech
 
     @abstractmethod
@@ -54,11 +57,8 @@ class BaseMetric(ABC):
         """The reference's call (base.py:41-43), extended to ragged batches: lists of 1-D
         utterances, or padded [B, L] tensors with per-row ``lengths`` (see batching.py)."""
         clean_speech, denoised_speech, lengths = self.split_ragged(clean_speech, denoised_speech, lengths)
-        if lengths is not None and self.sample_rate != self.EXPECTED_SAMPLING_RATE:
-            # the resampler must see each row zero-padded, as the row alone would be
-            clean_speech = zero_tail(clean_speech, lengths)
-            denoised_speech = zero_tail(denoised_speech, lengths)
-        clean_speech, denoised_speech = self.prepare_inputs(clean_speech, denoised_speech)
+        # with lengths, the resampler sees each row as the row alone would be (zeros past it)
+        clean_speech, denoised_speech = self.prepare_inputs(clean_speech, denoised_speech, lengths)
         if lengths is None:
             return self.compute_metric(clean_speech, denoised_speech)
         lengths = resampled_lengths(lengths, self.sample_rate, self.EXPECTED_SAMPLING_RATE)

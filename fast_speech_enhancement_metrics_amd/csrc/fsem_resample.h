@@ -13,10 +13,11 @@ struct ResampleKernel {
 
 int make_resample_kernel(int32_t orig_freq, int32_t new_freq, ResampleKernel *rk);
 
-// Tiled polyphase resampler for any rate pair (resample.hip): rows r of `in` (row length
-// lens[r] clamped to [0, n_in], or n_in) -> out + r * ld_out, ceil(n * nw / orig) samples.
+// Polyphase resampler for any rate pair (resample.hip): rows r of `in` (row length n = lens[r]
+// clamped to [0, n_in], or n_in) -> out + r * ld_out, ceil(n * nw / orig) samples; columns
+// [ceil(n * nw / orig), zc) are zeroed (zc <= ceil(n_in * nw / orig); 0: none).
 int launch_resample_tiled(const float *in, int64_t rows, int64_t n_in, int64_t ld_in, const int32_t *lens,
-                          float *out, int64_t ld_out, const ResampleKernel &rk, hipStream_t st);
+                          float *out, int64_t ld_out, int64_t zc, const ResampleKernel &rk, hipStream_t st);
 
 // One output sample o of a row x[0..n): torchaudio's pad + strided conv1d.
 __device__ __forceinline__ float resample_at(const float *__restrict__ x, int64_t n, int64_t o,

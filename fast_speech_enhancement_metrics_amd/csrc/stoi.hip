@@ -674,9 +674,9 @@ inline int run(const float *ref, const float *deg, int64_t B, int64_t length, in
                        nitems, w.y10, g.y_ld, w.vad, g.v_ld);
   } else if (g.mode == 2) {
     // other rates: tiled polyphase resampler into the 10 kHz rows, then the clean energies
-    rc = launch_resample_tiled(ref, B, length, ld, lengths, w.y10, 2 * g.y_ld, rk, st);
+    rc = launch_resample_tiled(ref, B, length, ld, lengths, w.y10, 2 * g.y_ld, 0, rk, st);
     if (rc != FSEM_OK) return rc;
-    rc = launch_resample_tiled(deg, B, length, ld, lengths, w.y10 + g.y_ld, 2 * g.y_ld, rk, st);
+    rc = launch_resample_tiled(deg, B, length, ld, lengths, w.y10 + g.y_ld, 2 * g.y_ld, 0, rk, st);
     if (rc != FSEM_OK) return rc;
     hipLaunchKernelGGL(stoi_vad10, dim3((unsigned)((g.L10 + VQ - 1) / VQ), (unsigned)B), dim3(256), 0, st, w.y10,
                        g.y_ld, rows, w.vad, g.v_ld);

@@ -44,7 +44,11 @@ class Resample(torch.nn.Module):
             return n
         return int(math.ceil(self.new * n / self.orig))
 
-    def forward(self, waveform: torch.Tensor) -> torch.Tensor:
+    def forward(self, waveform: torch.Tensor, lengths: torch.Tensor | None = None) -> torch.Tensor:
+        """[..., n] -> [..., ceil(new * n / orig)].  ``lengths`` ([rows] ints, rows = the flattened
+        leading dims): row r is resampled as its first lengths[r] samples alone (zeros past them)
+        and its output past ceil(new * lengths[r] / orig) is zero -- the zero-padded ragged rows of
+        BaseMetric.__call__ without materialising them."""
         if self.orig_freq == self.new_freq:
             return waveform
         shape = waveform.shape
@@ -56,10 +60,25 @@ class Resample(torch.nn.Module):
             n_out = self.output_length(n)
             out = torch.empty(x.shape[0], n_out, dtype=torch.float32, device=x.device)
             if x.shape[0] and n:
-                _native.check(lib.fsem_resample_f32(x.data_ptr(), x.shape[0], n, n, out.data_ptr(), n_out,
-                                                    self.orig_freq, self.new_freq,
-                                                    _native.stream_handle(x.device)), "resample")
+                st = _native.stream_handle(x.device)
+                if lengths is None:
+                    rc = lib.fsem_resample_f32(x.data_ptr(), x.shape[0], n, n, out.data_ptr(), n_out,
+                                               self.orig_freq, self.new_freq, st)
+                else:
+                    from .base import device_lengths
+                    lens = device_lengths(lengths, x.shape[0], n, x.device)
+                    rc = lib.fsem_resample_rows_f32(x.data_ptr(), x.shape[0], n, n, lens.data_ptr(),
+                                                    out.data_ptr(), n_out, self.orig_freq, self.new_freq, st)
+                _native.check(rc, "resample")
             return out.reshape(shape[:-1] + (n_out,))
+        if lengths is not None:
+            from .base import zero_tail
+            x = zero_tail(x, torch.as_tensor(lengths).reshape(-1))
+            res = self.forward(x)
+            t = torch.arange(res.shape[-1])
+            keep = t[None, :] < torch.as_tensor(
+                [self.output_length(int(v)) for v in torch.as_tensor(lengths).reshape(-1).tolist()])[:, None]
+            return torch.where(keep, res, torch.zeros((), dtype=res.dtype)).reshape(shape[:-1] + res.shape[-1:])
         xp = torch.nn.functional.pad(x.to(torch.float32), (self.width, self.width + self.orig))
         res = torch.nn.functional.conv1d(xp[:, None], self.kernel.to(xp.device), stride=self.orig)
         res = res.transpose(1, 2).reshape(x.shape[0], -1)[:, :self.output_length(n)]

@@ -55,6 +55,13 @@ int64_t fsem_resample_length(int64_t n_in, int32_t orig_freq, int32_t new_freq);
 int fsem_resample_f32(const float *in, int64_t rows, int64_t n_in, int64_t ld_in,
                       float *out, int64_t ld_out, int32_t orig_freq, int32_t new_freq,
                       void *stream);
+/* Ragged rows: row r is resampled as its first lengths[r] samples alone (zeros past them, as
+ * BaseMetric.__call__'s zero-padded rows), giving fsem_resample_length(lengths[r], ...) samples;
+ * the rest of the row, up to fsem_resample_length(n_in, ...), is written as zeros.
+ * FSEM_ERATE if orig_freq == new_freq. */
+int fsem_resample_rows_f32(const float *in, int64_t rows, int64_t n_in, int64_t ld_in,
+                           const int32_t *lengths, float *out, int64_t ld_out, int32_t orig_freq,
+                           int32_t new_freq, void *stream);
 
 /* ---------------------------------------------------------------- PESQ-wb
  * Whole-metric entry: replaces PESQ.compute_metric    fast_se_metrics/PESQ.py:232-245

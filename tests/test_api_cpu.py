@@ -106,3 +106,21 @@ def test_cpu_resampler_matches_reference_vectors():
     g = load_golden("stoi_16k")
     out = Resample(16000, 10000)(torch.from_numpy(g["clean_f"])).numpy()
     np.testing.assert_allclose(out, g["x10_clean"], atol=2e-6, rtol=0)
+
+
+def test_cpu_resampler_ragged_rows():
+    """Resample.forward(x, lengths) on CPU: each row as the row alone, zero past its output length."""
+    from fast_speech_enhancement_metrics_amd.resample import Resample
+    from oracle import ta
+    rng = np.random.default_rng(3)
+    x = rng.standard_normal((4, 1003)).astype(np.float32)
+    lens = [1003, 500, 7, 0]
+    for orig, new in ((8000, 16000), (8000, 10000)):
+        m = Resample(orig, new)
+        out = m(torch.from_numpy(x), torch.tensor(lens)).numpy()
+        assert out.shape == (4, m.output_length(1003))
+        for r, ln in enumerate(lens):
+            k = m.output_length(ln)
+            if ln:
+                np.testing.assert_allclose(out[r, :k], ta.resample(x[r:r + 1, :ln], orig, new)[0], atol=2e-6)
+            assert (out[r, k:] == 0).all()
