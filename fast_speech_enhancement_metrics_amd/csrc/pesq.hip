@@ -247,15 +247,80 @@ __device__ __forceinline__ float iir_pass2_masked(float4 *__restrict__ w4, float
   return acc;
 }
 
+// Band-pass section k of iir_pass2_group, one sample (same operations, same order).
+__device__ __forceinline__ float bp_section(int k, float u, float z[NS]) {
+  const float y = u + z[2 * k];
+  z[2 * k] = fmaf(-kBpSecA[k][0], y, z[2 * k + 1]);
+  z[2 * k + 1] = fmaf(-kBpSecA[k][1], y, -u);
+  return y;
+}
+
+// One time-skewed step of the cascade: section k (KLO <= k <= KHI) works on sample n - k, its
+// input p[k] being section k-1's output of the previous step, so the five section updates of a
+// step are independent (a lone wave runs a dependent v_fma chain at ~1.7x the time per
+// instruction of independent ones, tools/micro/dep_chain.hip).  Section 4's output feeds acc.
+template <int KLO, int KHI>
+__device__ __forceinline__ void bp_step(float x, float p[5], float z[NS], float &acc) {
+#pragma unroll
+  for (int k = KHI; k >= KLO; --k) {  // descending: p[k+1] is read before section k rewrites it
+    const float y = bp_section(k, k == 0 ? x : p[k], z);
+    if (k < 4) p[k + 1] = y;
+    else acc = fmaf(y, y, acc);
+  }
+}
+
+// Pre-emphasis of one untapered sample (iir_pass2_group's second filter).
+__device__ __forceinline__ float pre_step(float xp, float z[NS]) {
+  const float y = fmaf(kPreB[0], xp, z[NBP]);
+  z[NBP] = fmaf(kPreB[1], xp, fmaf(-kPreA[1], y, z[NBP + 1]));
+  z[NBP + 1] = fmaf(kPreB[2], xp, -kPreA[2] * y);
+  return y;
+}
+
+// Steady-state group q of the skewed pass: all five sections active; the power of group q-1
+// goes to acc.
+__device__ __forceinline__ void skew_group(float4 *__restrict__ w4, int q, float p[5], float z[NS], float &acc) {
+  const float4 v = w4[q];
+  float xs[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    bp_step<0, 4>(xs[c], p, z, acc);
+    xs[c] = pre_step(xs[c], z);
+  }
+  w4[q] = make_float4(xs[0], xs[1], xs[2], xs[3]);
+}
+
 // Unmasked: the owned power of a lane whose range boundaries lie at 0, P_HI, P_LO or CH.
+// The cascade runs time-skewed (bp_step): bitwise the per-sample arithmetic and summation order
+// of iir_pass2_group<false, false>, with four fill steps in group 0 and four drain steps after
+// group CH/4-1; the power of group r is summed while group r+1 is filtered.
+static_assert(P_HI >= 4, "group 0 lies in the first power part");
 __device__ __forceinline__ float iir_pass2_split(float4 *__restrict__ w4, float z[NS], int own_lo, int own_hi) {
   float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+  float p[5];
+  {
+    const float4 v = w4[0];
+    float xs[4] = {v.x, v.y, v.z, v.w};
+    bp_step<0, 0>(xs[0], p, z, a0);
+    xs[0] = pre_step(xs[0], z);
+    bp_step<0, 1>(xs[1], p, z, a0);
+    xs[1] = pre_step(xs[1], z);
+    bp_step<0, 2>(xs[2], p, z, a0);
+    xs[2] = pre_step(xs[2], z);
+    bp_step<0, 3>(xs[3], p, z, a0);
+    xs[3] = pre_step(xs[3], z);
+    w4[0] = make_float4(xs[0], xs[1], xs[2], xs[3]);
+  }
 #pragma unroll
-  for (int q = 0; q < P_HI / 4; ++q) iir_pass2_group<false, false>(w4, q, z, a0, 0, 0, 0, 0.f, 0.f);
+  for (int q = 1; q < P_HI / 4 + 1; ++q) skew_group(w4, q, p, z, a0);
 #pragma unroll 3
-  for (int q = P_HI / 4; q < P_LO / 4; ++q) iir_pass2_group<false, false>(w4, q, z, a1, 0, 0, 0, 0.f, 0.f);
+  for (int q = P_HI / 4 + 1; q < P_LO / 4 + 1; ++q) skew_group(w4, q, p, z, a1);
 #pragma unroll
-  for (int q = P_LO / 4; q < CH / 4; ++q) iir_pass2_group<false, false>(w4, q, z, a2, 0, 0, 0, 0.f, 0.f);
+  for (int q = P_LO / 4 + 1; q < CH / 4; ++q) skew_group(w4, q, p, z, a2);
+  bp_step<1, 4>(0.f, p, z, a2);
+  bp_step<2, 4>(0.f, p, z, a2);
+  bp_step<3, 4>(0.f, p, z, a2);
+  bp_step<4, 4>(0.f, p, z, a2);
   const bool lo_in = own_lo <= 0, hi_in = own_hi >= CH;
   return (lo_in && hi_in) ? (a0 + a1) + a2
        : (own_lo == P_LO && hi_in) ? a2
