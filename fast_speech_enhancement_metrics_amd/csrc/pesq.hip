@@ -1021,7 +1021,10 @@ __global__ void __launch_bounds__(BT) __attribute__((amdgpu_waves_per_eu(4)))
     const double ds = sqrt(as_ / nw), da = sqrt(aa_ / nw);
     double m = 4.5 - 0.1 * ds - 0.0309 * da;              // PESQ.py:240
     m = 0.999 + 4.0 / (1.0 + exp(-1.3669 * m + 3.8224));  // PESQ.py:243
-    mos[b] = (float)m;
+    // a signal with zero (or non-finite) band-pass power: the reference's x * sqrt(1e7 / power)
+    // (PESQ.py:100) turns it into NaN samples, which torch's clamp / pow propagate to the score;
+    // here the scale multiplies Bark bands whose NaNs the comparisons above would drop
+    mos[b] = (__builtin_isfinite(sc) && __builtin_isfinite(sn)) ? (float)m : __builtin_nanf("");
   }
 }
 

@@ -124,3 +124,19 @@ def test_cpu_resampler_ragged_rows():
             if ln:
                 np.testing.assert_allclose(out[r, :k], ta.resample(x[r:r + 1, :ln], orig, new)[0], atol=2e-6)
             assert (out[r, k:] == 0).all()
+
+
+def test_cpu_mode_zero_denoised_signal():
+    """use_gpu=False on an all-zero denoised signal: PESQ NaN (the level alignment divides by a
+    zero power, PESQ.py:98-101, and torch's clamp keeps the NaN), STOI/ESTOI 0 (zero-variance rows
+    normalise to 0: the build's deterministic choice for STOI.py:116)."""
+    import warnings
+    from fast_speech_enhancement_metrics_amd import PESQ, STOI
+    from fast_speech_enhancement_metrics_amd.synthetic import speech_like_pairs
+    c, n, _ = speech_like_pairs(2, 48000, 16000, seed=5)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        p = PESQ(16000)(c, torch.zeros_like(n))
+        s = STOI(16000)(c, torch.zeros_like(n))
+    assert all(np.isnan(r["PESQ"]) for r in p)
+    assert all(r["STOI"] == 0.0 and r["ESTOI"] == 0.0 for r in s)
