@@ -388,6 +388,8 @@ __global__ void __launch_bounds__(64 * TOB_WAVES)
     // correlation (an all-zero denoised signal would score ~0.8 instead of 0).
     const bool c_zero = !__any(v[0].r != 0.f || v[1].r != 0.f || v[2].r != 0.f || v[3].r != 0.f);
     const bool d_zero = !__any(v[0].i != 0.f || v[1].i != 0.f || v[2].i != 0.f || v[3].i != 0.f);
+    // wave-uniform factors (SGPR operands of the final multiply): 0.25, or 0 for a zero frame
+    const float c_scale = c_zero ? 0.f : 0.25f, d_scale = d_zero ? 0.f : 0.25f;
     fft512_wave(v, wbuf, lane, tw1, tw2);
     float pc[4], pd[4];
 #pragma unroll
@@ -399,8 +401,8 @@ __global__ void __launch_bounds__(64 * TOB_WAVES)
         mi = v[(8 - r) & 7].i;
       }
       const float zr = v[r].r, zi = v[r].i;
-      pc[r] = c_zero ? 0.f : 0.25f * fmaf(zr + mr, zr + mr, (zi - mi) * (zi - mi));  // explicit: no contraction choice
-      pd[r] = d_zero ? 0.f : 0.25f * fmaf(zi + mi, zi + mi, (zr - mr) * (zr - mr));
+      pc[r] = c_scale * fmaf(zr + mr, zr + mr, (zi - mi) * (zi - mi));  // explicit: no contraction choice
+      pd[r] = d_scale * fmaf(zi + mi, zi + mi, (zr - mr) * (zr - mr));
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
