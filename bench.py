@@ -255,9 +255,7 @@ def run_c5(args, world, rank, dev, distributed):
     ranks by LPT over their 16 kHz-equivalent length (distributed.lpt_shards)."""
     import numpy as np
     from fast_speech_enhancement_metrics_amd import PESQ, PESQ_STOI, STOI
-    from fast_speech_enhancement_metrics_amd.batching import resampled_lengths
     from fast_speech_enhancement_metrics_amd.distributed import lpt_shards
-    from fast_speech_enhancement_metrics_amd.resample import Resample
     from fast_speech_enhancement_metrics_amd.synthetic import speech_like_pairs
 
     n_total = 2048 * world
@@ -280,14 +278,12 @@ def run_c5(args, world, rank, dev, distributed):
         groups[sr] = (torch.cat(cs), torch.cat(ns), torch.from_numpy(ln.astype(np.int32)).to(dev))
     joint = PESQ_STOI(16000, use_gpu=True)
     p8, s8 = PESQ(8000, use_gpu=True), STOI(8000, use_gpu=True)
-    up = Resample(8000, 16000).to(dev)
 
     def step():
         c, n, l16 = groups[16000]
         out16 = torch.stack(joint.scores(c, n, lengths=l16), 1)
         c8, n8, l8 = groups[8000]
-        l8to16 = resampled_lengths(l8, 8000, 16000).to(dev)
-        mos8 = p8.scores(up(c8, l8), up(n8, l8), lengths=l8to16)  # each row resampled as the row alone
+        mos8 = p8.scores(c8, n8, lengths=l8, sample_rate=8000)  # 8 -> 16 kHz, each row as the row alone
         st8, es8 = s8.scores(c8, n8, 8000, lengths=l8)
         out8 = torch.stack([mos8, st8, es8], 1)
         res = torch.cat([out8, out16])

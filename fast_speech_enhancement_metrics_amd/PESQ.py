@@ -10,7 +10,7 @@ from __future__ import annotations
 import torch
 
 from . import _cpu, _native
-from .base import BaseMetric, as_rows, device_lengths
+from .base import BaseMetric, as_rows, check_row_rate, device_lengths, noisy_shape, resample_rows
 
 
 class PESQ(BaseMetric):
@@ -21,12 +21,23 @@ class PESQ(BaseMetric):
         super().__init__(sample_rate, use_gpu)
 
     # ------------------------------------------------------------------ device paths
-    def scores(self, clean_speech: torch.Tensor, denoised_speech: torch.Tensor, lengths=None) -> torch.Tensor:
+    def scores(self, clean_speech: torch.Tensor, denoised_speech: torch.Tensor, lengths=None,
+               sample_rate: int | None = None) -> torch.Tensor:
         """Per-utterance MOS as a tensor on the metric's device (no host sync on GPU).
 
-        16 kHz rows.  ``lengths`` (optional, [B] ints): row b holds lengths[b] samples and scores
-        as the reference would on that unpadded row alone; rows under 20 frames give NaN.
+        Rows at ``sample_rate``; None means rows already at 16 kHz, which requires a 16 kHz metric
+        (a ``PESQ(8000)`` must be told its rows' rate, or it would score them as 16 kHz).  Other
+        rates are resampled to 16 kHz first, each row as the row alone (BaseMetric.prepare_audio,
+        base.py:19-20).  ``lengths`` (optional, [B] ints at that rate): row b holds lengths[b]
+        samples and scores as the reference would on that unpadded row alone; rows under 20
+        frames give NaN.
         """
+        sr = check_row_rate(self, sample_rate)
+        if noisy_shape(clean_speech) != noisy_shape(denoised_speech):
+            raise Exception("`clean_speech` and `denoised_speech` should have the same shape.")
+        if sr != self.EXPECTED_SAMPLING_RATE:
+            clean_speech, denoised_speech, lengths = resample_rows(clean_speech, denoised_speech, lengths, sr,
+                                                                   self.EXPECTED_SAMPLING_RATE)
         clean = as_rows(clean_speech)
         noisy = as_rows(denoised_speech)
         B, L = clean.shape
@@ -59,5 +70,5 @@ class PESQ(BaseMetric):
                        lengths=None) -> list[dict[str, float]]:
         assert clean_speech is not None
         with torch.inference_mode():
-            mos = self.scores(clean_speech, denoised_speech, lengths)
+            mos = self.scores(clean_speech, denoised_speech, lengths, sample_rate=self.EXPECTED_SAMPLING_RATE)
             return [{"PESQ": m} for m in mos.tolist()]

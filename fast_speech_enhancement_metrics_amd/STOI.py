@@ -12,7 +12,7 @@ import warnings
 import torch
 
 from . import _cpu, _native
-from .base import BaseMetric, as_rows, device_lengths, zero_tail
+from .base import BaseMetric, as_rows, check_row_rate, device_lengths, zero_tail
 from .batching import resampled_lengths
 
 
@@ -36,10 +36,11 @@ class STOI(BaseMetric):
                lengths=None):
         """(stoi[B], estoi[B]) tensors on the metric's device; NaN where no segment exists.
 
-        Rows at ``sample_rate`` (default 10 kHz).  ``lengths`` (optional, [B] ints at that rate):
+        Rows at ``sample_rate``; None means rows already at 10 kHz, which requires a 10 kHz metric
+        (``STOI(16000).scores`` must be told its rows' rate).  ``lengths`` (optional, [B] ints at that rate):
         row b holds lengths[b] samples and scores as the reference would on the unpadded row.
         """
-        sr = self.EXPECTED_SAMPLING_RATE if sample_rate is None else int(sample_rate)
+        sr = check_row_rate(self, sample_rate)
         clean = as_rows(clean_speech)
         noisy = as_rows(denoised_speech)
         if noisy.shape != clean.shape:
@@ -66,7 +67,8 @@ class STOI(BaseMetric):
         e = torch.empty(B, dtype=torch.float32, device=clean.device)
         nbytes = lib.fsem_stoi_workspace_bytes(B, L, sr)
         if nbytes == 0:
-            raise NotImplementedError(f"unsupported sample rate {sr} for the fused STOI resampler")
+            raise NotImplementedError(f"unsupported sample rate {sr}: its resampling filter to 10 kHz would be longer "
+                                      "than 8192 taps (include/fsem.h, FSEM_ERATE)")
         ws = _native.workspace(nbytes, clean.device)
         rc = lib.fsem_stoi_f32(clean.data_ptr(), noisy.data_ptr(), B, L, clean.stride(0),
                                lens.data_ptr() if lens is not None else None, sr, s.data_ptr(),
@@ -93,7 +95,8 @@ class STOI(BaseMetric):
                        lengths=None) -> list[dict[str, float]]:
         assert clean_speech is not None
         with torch.no_grad():
-            return self._finish(*self.scores(clean_speech, denoised_speech, lengths=lengths))
+            return self._finish(*self.scores(clean_speech, denoised_speech, self.EXPECTED_SAMPLING_RATE,
+                                             lengths=lengths))
 
     def __call__(self, clean_speech, denoised_speech, lengths=None) -> list[dict[str, float]]:
         if self.device == "cuda" and clean_speech is not None:

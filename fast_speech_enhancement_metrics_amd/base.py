@@ -103,3 +103,36 @@ def as_rows(x: torch.Tensor) -> torch.Tensor:
     if x.dim() != 2 or x.stride(-1) != 1 or x.stride(0) < x.shape[1]:
         x = x.reshape(-1, x.shape[-1]).contiguous()
     return x
+
+
+def noisy_shape(x) -> tuple:
+    return tuple(torch.atleast_2d(torch.as_tensor(x)).shape) if x is not None else ()
+
+
+def check_row_rate(metric, sample_rate: int | None) -> int:
+    """Rate of the rows handed to ``metric.scores``.  None means the metric's expected rate, which
+    is only unambiguous when the metric was constructed for that rate: a metric built for another
+    rate must be told (otherwise its rows would silently be scored at the wrong rate)."""
+    if sample_rate is None:
+        if metric.sample_rate != metric.EXPECTED_SAMPLING_RATE:
+            raise ValueError(f"{type(metric).__name__}({metric.sample_rate}).scores: pass sample_rate= (the rate of "
+                             f"the rows; {metric.EXPECTED_SAMPLING_RATE} if they are already resampled)")
+        return int(metric.EXPECTED_SAMPLING_RATE)
+    return int(sample_rate)
+
+
+def resample_rows(clean, noisy, lengths, orig: int, new: int):
+    """(clean, noisy, lengths) resampled orig -> new, each row as the row alone when ``lengths`` is
+    given (BaseMetric.prepare_audio, base.py:19-20); lengths become the resampled lengths."""
+    rs = Resample(orig, new)
+    noisy = torch.atleast_2d(noisy)
+    if noisy.is_cuda:
+        rs = rs.to(noisy.device)
+    lens = None
+    if lengths is not None:
+        lens = device_lengths(lengths, noisy.shape[0], noisy.shape[-1], noisy.device)
+    clean = rs(torch.atleast_2d(clean), lens) if clean is not None else None
+    noisy = rs(noisy, lens)
+    if lens is not None:
+        lens = resampled_lengths(lens, orig, new).to(noisy.device)
+    return clean, noisy, lens

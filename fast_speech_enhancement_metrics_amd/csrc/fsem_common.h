@@ -100,4 +100,8 @@ __device__ __forceinline__ void lds_stores_done() { asm volatile("s_waitcnt lgkm
 
 static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// Launches that map rows (utterances) to grid.y cover at most kMaxGridY rows each; the host loops
+// over slices [r0, r0 + kMaxGridY) and passes r0 (HIP's grid.y limit, hipDeviceProp maxGridSize[1]).
+constexpr int64_t kMaxGridY = 65535;
+
 }  // namespace fsem

@@ -32,6 +32,8 @@
 // pesq_back   one 256-thread workgroup per utterance: level scale, silent frames, band and
 //   frame equalisation, Zwicker loudness, symmetric / asymmetric disturbance, L6/L2 pooling
 //   and the MOS mapping (PESQ.py:142-245), deterministic block reductions.
+#include <stdlib.h>
+
 #include <algorithm>
 #include <mutex>
 
@@ -1068,7 +1070,13 @@ int fsem::pesq::launch_front(const float *ref, const float *deg, int64_t batch, 
   const int64_t nitems = 2 * batch * (int64_t)g.nseg;
   int dev = 0, ncu = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-  const int64_t grid = std::min<int64_t>(nitems, (int64_t)ncu * 2);  // 2 resident workgroups per CU
+  // 2 resident workgroups per CU; FSEM_FRONT_WGS_PER_CU (diagnostics only) overrides
+  static const int wgs_per_cu = [] {
+    const char *e = getenv("FSEM_FRONT_WGS_PER_CU");
+    const int v = e ? atoi(e) : 0;
+    return (v >= 1 && v <= 2) ? v : 2;
+  }();
+  const int64_t grid = std::min<int64_t>(nitems, (int64_t)ncu * wgs_per_cu);
   float *ppart = static_cast<float *>(ws);
 #define FSEM_FRONT(J, V)                                                                                \
   hipLaunchKernelGGL((pesq::pesq_front<J, V>), dim3((unsigned)grid), dim3(pesq::PT), 0, st, ref, deg, batch, \

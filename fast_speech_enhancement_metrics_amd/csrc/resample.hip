@@ -26,25 +26,15 @@ int make_resample_kernel(int32_t orig_freq, int32_t new_freq, ResampleKernel *rk
   const double base = (double)(orig < nw ? orig : nw) * 0.99;
   const int width = (int)ceil(6.0 * orig / base);
   const int taps = 2 * width + orig;
-  if ((int64_t)nw * taps > FSEM_RS_MAX_COEF) return FSEM_ERATE;
+  if (taps > RS_BIG_TAPS) return FSEM_ERATE;  // reduced input rate too large (see fsem.h)
   rk->orig = orig;
   rk->nw = nw;
   rk->taps = taps;
   rk->width = width;
-  const double pi = 3.14159265358979323846;
-  for (int j = 0; j < nw; ++j) {
-    const float ph32 = (float)(-j) / (float)nw;  // int arange / int -> float32 in torchaudio
-    for (int t = 0; t < taps; ++t) {
-      double tt = ((double)ph32 + (double)(t - width) / orig) * base;
-      if (tt < -6.0) tt = -6.0;
-      if (tt > 6.0) tt = 6.0;
-      const double c = cos(tt * pi / 6.0 / 2.0);
-      const double win = c * c;
-      tt *= pi;
-      const double s = (tt == 0.0) ? 1.0 : sin(tt) / tt;
-      rk->k[j * taps + t] = (float)(s * (win * (base / orig)));
-    }
-  }
+  rk->big = (int64_t)nw * taps > FSEM_RS_MAX_COEF;
+  if (rk->big) return FSEM_OK;  // coefficients built on the device (resample_sinc_lds)
+  for (int j = 0; j < nw; ++j)
+    for (int t = 0; t < taps; ++t) rk->k[j * taps + t] = sinc_coef(j, t, orig, nw, width);
   return FSEM_OK;
 }
 
@@ -57,12 +47,12 @@ constexpr int RS_T = 256;
 constexpr int RS_XS = 8192 + FSEM_RS_MAX_COEF;  // staged inputs: GT*orig + taps <= this
 __global__ void __launch_bounds__(RS_T) resample_tiled(const float *__restrict__ in, int64_t n_in, int64_t ld_in,
                                                       const int32_t *__restrict__ lens, float *__restrict__ out,
-                                                      int64_t ld_out, int64_t zc, int gt, ResampleKernel rk) {
+                                                      int64_t ld_out, int64_t zc, int gt, int64_t r0, ResampleKernel rk) {
   __shared__ float xs[RS_XS];
   __shared__ float ks[FSEM_RS_MAX_COEF];
   __shared__ float ys[RS_T * 8];
   const int tid = threadIdx.x;
-  const int64_t r = blockIdx.y;
+  const int64_t r = r0 + blockIdx.y;
   int64_t n = n_in;
   if (lens) {
     const int64_t v = lens[r];
@@ -118,11 +108,11 @@ __global__ void __launch_bounds__(RS_T) resample_tiled(const float *__restrict__
 template <int ORIG, int NW, int TAPS>
 __global__ void __launch_bounds__(RS_T) resample_tiled_t(const float *__restrict__ in, int64_t n_in, int64_t ld_in,
                                                         const int32_t *__restrict__ lens, float *__restrict__ out,
-                                                        int64_t ld_out, int64_t zc, int gt, ResampleKernel rk) {
+                                                        int64_t ld_out, int64_t zc, int gt, int64_t r0, ResampleKernel rk) {
   __shared__ float xs[RS_XS];
   __shared__ float ys[RS_T * 8];
   const int tid = threadIdx.x;
-  const int64_t r = blockIdx.y;
+  const int64_t r = r0 + blockIdx.y;
   int64_t n = n_in;
   if (lens) {
     const int64_t v = lens[r];
@@ -181,13 +171,13 @@ __global__ void __launch_bounds__(RS_T) resample_tiled_t(const float *__restrict
 template <int ORIG, int NW, int TAPS, int G>
 __global__ void __launch_bounds__(RS_T) resample_direct_t(const float *__restrict__ in, int64_t n_in, int64_t ld_in,
                                                          const int32_t *__restrict__ lens, float *__restrict__ out,
-                                                         int64_t ld_out, int64_t zc, ResampleKernel rk) {
+                                                         int64_t ld_out, int64_t zc, int64_t r0, ResampleKernel rk) {
   constexpr int W = (TAPS - ORIG) / 2;                 // rk.width
   constexpr int W4 = (W + 3) & ~3;                     // first chunk starts W4 before the group
   constexpr int NCH = ((G - 1) * ORIG + TAPS + (W4 - W) + 3) / 4;
   constexpr int NO = G * NW;
   static_assert((G * ORIG) % 4 == 0 && NO % 4 == 0, "float4 granularity");
-  const int64_t r = blockIdx.y;
+  const int64_t r = r0 + blockIdx.y;
   int64_t n = n_in;
   if (lens) {
     const int64_t v = lens[r];
@@ -246,17 +236,85 @@ __global__ void __launch_bounds__(RS_T) resample_direct_t(const float *__restric
   }
 }
 
-int launch_resample_tiled(const float *in, int64_t rows, int64_t n_in, int64_t ld_in, const int32_t *lens,
-                          float *out, int64_t ld_out, int64_t zc, const ResampleKernel &rk, hipStream_t st) {
-  if (rows <= 0 || n_in <= 0) return FSEM_OK;
-  if (rows > 65535) return FSEM_EINVAL;
-  const bool vec = ((uintptr_t)in % 16 == 0) && ((uintptr_t)out % 16 == 0) && ld_in % 4 == 0 && ld_out % 4 == 0;
+// Large coefficient tables (nw * taps > FSEM_RS_MAX_COEF: 44.1 kHz, 22.05 kHz, 11.025 kHz ... to
+// 16 or 10 kHz).  A workgroup owns the phases [j0, j0 + J) of the polyphase groups [m0, m0 + GM):
+// it builds those J coefficient rows in LDS with sinc_coef (the host formula, evaluated in float64
+// on the device) and stages the GM groups' input window, then each thread evaluates outputs
+// (group, phase) with the same k-ordered fmaf chain as resample_at.  Consecutive threads take
+// consecutive phases of one group: coalesced stores of the interleaved output.
+constexpr int RS_BIG_K = 8192;  // coefficient floats staged per workgroup
+constexpr int RS_BIG_X = 8192;  // input floats staged per workgroup
+__global__ void __launch_bounds__(RS_T) resample_sinc_lds(const float *__restrict__ in, int64_t n_in, int64_t ld_in,
+                                                         const int32_t *__restrict__ lens, float *__restrict__ out,
+                                                         int64_t ld_out, int64_t zc, int64_t r0, int njb, int J,
+                                                         int GM, int orig, int nw, int taps, int width) {
+  __shared__ float ks[RS_BIG_K];
+  __shared__ float xs[RS_BIG_X];
+  const int tid = threadIdx.x;
+  const int64_t r = r0 + blockIdx.y;
+  int64_t n = n_in;
+  if (lens) {
+    const int64_t v = lens[r];
+    n = v < 0 ? 0 : (v > n_in ? n_in : v);
+  }
+  const int64_t n_out = (n * nw + orig - 1) / orig;
+  const int jb = (int)(blockIdx.x % (unsigned)njb);
+  const int64_t m0 = (int64_t)(blockIdx.x / (unsigned)njb) * GM;
+  const int j0 = jb * J, nj = min(J, nw - j0);
+  float *__restrict__ y = out + r * ld_out;
+  if (m0 * nw >= n_out) {  // past the row: only the zero tail [n_out, zc)
+    for (int i = tid; i < GM * nj; i += RS_T) {
+      const int64_t o = (m0 + i / nj) * nw + j0 + i % nj;
+      if (o < zc) y[o] = 0.f;
+    }
+    return;
+  }
+  for (int i = tid; i < nj * taps; i += RS_T) ks[i] = sinc_coef(j0 + i / taps, i % taps, orig, nw, width);
+  const float *__restrict__ x = in + r * ld_in;
+  const int64_t base = m0 * orig - width;
+  const int nx = (GM - 1) * orig + taps;
+  for (int i = tid; i < nx; i += RS_T) {
+    const int64_t t = base + i;
+    xs[i] = (t >= 0 && t < n) ? x[t] : 0.f;
+  }
+  __syncthreads();
+  for (int i = tid; i < GM * nj; i += RS_T) {
+    const int g = i / nj, jj = i % nj;
+    const int64_t o = (m0 + g) * nw + j0 + jj;
+    const float *__restrict__ kj = ks + jj * taps;
+    const float *__restrict__ xg = xs + g * orig;
+    float acc = 0.f;
+    for (int t = 0; t < taps; ++t) acc = fmaf(kj[t], xg[t], acc);
+    if (o < n_out)
+      y[o] = acc;
+    else if (o < zc)
+      y[o] = 0.f;
+  }
+}
+static_assert(RS_BIG_TAPS <= RS_BIG_K && RS_BIG_TAPS <= RS_BIG_X, "one phase row and one group window fit");
+
+// One launch over rows [r0, r0 + nrows) (nrows <= kMaxGridY).
+static int launch_resample_slice(const float *in, int64_t nrows, int64_t r0, int64_t n_in, int64_t ld_in,
+                                 const int32_t *lens, float *out, int64_t ld_out, int64_t zc, const ResampleKernel &rk,
+                                 hipStream_t st) {
+  const int64_t rows = nrows;
   const int64_t groups = (n_in + rk.orig - 1) / rk.orig + 1;
+  if (rk.big) {  // large coefficient tables (e.g. 44.1 kHz): built per workgroup in LDS
+    const int J = std::min(rk.nw, std::max(1, RS_BIG_K / rk.taps));
+    const int GM = std::max(1, (RS_BIG_X - rk.taps) / rk.orig + 1);
+    const int64_t njb = (rk.nw + J - 1) / J, nmb = (groups + GM - 1) / GM;
+    if ((double)njb * (double)nmb > 2147483647.0) return FSEM_EINVAL;
+    hipLaunchKernelGGL(resample_sinc_lds, dim3((unsigned)(njb * nmb), (unsigned)rows), dim3(RS_T), 0, st, in, n_in,
+                       ld_in, lens, out, ld_out, zc, r0, (int)njb, J, GM, rk.orig, rk.nw, rk.taps, rk.width);
+    FSEM_CHECK_LAUNCH();
+    return FSEM_OK;
+  }
+  const bool vec = ((uintptr_t)in % 16 == 0) && ((uintptr_t)out % 16 == 0) && ld_in % 4 == 0 && ld_out % 4 == 0;
 #define FSEM_RS_DIRECT(O, N, T, G)                                                                           \
   if (vec && rk.orig == O && rk.nw == N && rk.taps == T) {                                                   \
     const dim3 grid_d((unsigned)((groups + RS_T * G - 1) / (RS_T * G)), (unsigned)rows);                    \
     hipLaunchKernelGGL((resample_direct_t<O, N, T, G>), grid_d, dim3(RS_T), 0, st, in, n_in, ld_in, lens, out, \
-                       ld_out, zc, rk);                                                                          \
+                       ld_out, zc, r0, rk);                                                                      \
     FSEM_CHECK_LAUNCH();                                                                                     \
     return FSEM_OK;                                                                                          \
   }
@@ -270,7 +328,7 @@ int launch_resample_tiled(const float *in, int64_t rows, int64_t n_in, int64_t l
 #define FSEM_RS_CASE(O, N, T)                                                                                \
   if (rk.orig == O && rk.nw == N && rk.taps == T) {                                                          \
     hipLaunchKernelGGL((resample_tiled_t<O, N, T>), grid, dim3(RS_T), 0, st, in, n_in, ld_in, lens, out, ld_out, \
-                       zc, gt, rk);                                                                               \
+                       zc, gt, r0, rk);                                                                           \
     FSEM_CHECK_LAUNCH();                                                                                      \
     return FSEM_OK;                                                                                           \
   }
@@ -278,8 +336,19 @@ int launch_resample_tiled(const float *in, int64_t rows, int64_t n_in, int64_t l
   FSEM_RS_CASE(4, 5, 18)   // 8 -> 10 kHz (STOI at 8 kHz)
   FSEM_RS_CASE(3, 1, 41)   // 48 -> 16 kHz
 #undef FSEM_RS_CASE
-  hipLaunchKernelGGL(resample_tiled, grid, dim3(RS_T), 0, st, in, n_in, ld_in, lens, out, ld_out, zc, gt, rk);
+  hipLaunchKernelGGL(resample_tiled, grid, dim3(RS_T), 0, st, in, n_in, ld_in, lens, out, ld_out, zc, gt, r0, rk);
   FSEM_CHECK_LAUNCH();
+  return FSEM_OK;
+}
+
+int launch_resample_tiled(const float *in, int64_t rows, int64_t n_in, int64_t ld_in, const int32_t *lens,
+                          float *out, int64_t ld_out, int64_t zc, const ResampleKernel &rk, hipStream_t st) {
+  if (rows <= 0 || n_in <= 0) return FSEM_OK;
+  for (int64_t r0 = 0; r0 < rows; r0 += kMaxGridY) {
+    const int rc = launch_resample_slice(in, std::min(rows - r0, kMaxGridY), r0, n_in, ld_in, lens, out, ld_out, zc,
+                                         rk, st);
+    if (rc != FSEM_OK) return rc;
+  }
   return FSEM_OK;
 }
 
@@ -301,7 +370,7 @@ extern "C" int fsem_resample_f32(const float *in, int64_t rows, int64_t n_in, in
   int rc = fsem::make_resample_kernel(orig_freq, new_freq, &rk);
   if (rc != FSEM_OK) return rc;
   const int64_t n_out = (rk.nw * n_in + rk.orig - 1) / rk.orig;
-  if (ld_out < n_out || rows > 65535) return FSEM_EINVAL;
+  if (ld_out < n_out) return FSEM_EINVAL;
   return fsem::launch_resample_tiled(in, rows, n_in, ld_in, nullptr, out, ld_out, 0, rk, (hipStream_t)stream);
 }
 
@@ -315,6 +384,6 @@ extern "C" int fsem_resample_rows_f32(const float *in, int64_t rows, int64_t n_i
   int rc = fsem::make_resample_kernel(orig_freq, new_freq, &rk);
   if (rc != FSEM_OK) return rc;
   const int64_t n_out = (rk.nw * n_in + rk.orig - 1) / rk.orig;
-  if (ld_out < n_out || rows > 65535) return FSEM_EINVAL;
+  if (ld_out < n_out) return FSEM_EINVAL;
   return fsem::launch_resample_tiled(in, rows, n_in, ld_in, lengths, out, ld_out, n_out, rk, (hipStream_t)stream);
 }

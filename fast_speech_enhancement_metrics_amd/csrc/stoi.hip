@@ -207,11 +207,10 @@ constexpr int YT3 = VF3 * 128 + 128;
 __global__ void __launch_bounds__(256)
     stoi_resample_vad(const float *__restrict__ ref, const float *__restrict__ deg, Rows rows, int64_t ld,
                       int mode, ResampleKernel rk, float *__restrict__ y10, int64_t y_ld,
-                      float2 *__restrict__ vad, int64_t v_ld) {
+                      float2 *__restrict__ vad, int64_t v_ld, int64_t b0) {
   __shared__ __attribute__((aligned(16))) float ytile[YT3];
   const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar branches)
-  const int64_t b = blockIdx.y;
+  const int64_t b = b0 + blockIdx.y;
   const int64_t o0 = (int64_t)blockIdx.x * (VF3 * 128);
   const int64_t n_in = rows.n(b), L10 = rows.l10(b);
   if (o0 >= L10) return;
@@ -235,8 +234,9 @@ __global__ void __launch_bounds__(256)
 // quarter sums, 4096 samples per workgroup.
 constexpr int VQ = 4096;
 __global__ void __launch_bounds__(256)
-    stoi_vad10(const float *__restrict__ y10, int64_t y_ld, Rows rows, float2 *__restrict__ vad, int64_t v_ld) {
-  const int64_t b = blockIdx.y;
+    stoi_vad10(const float *__restrict__ y10, int64_t y_ld, Rows rows, float2 *__restrict__ vad, int64_t v_ld,
+               int64_t b0) {
+  const int64_t b = b0 + blockIdx.y;
   const int64_t o0 = (int64_t)blockIdx.x * VQ;
   const int64_t L10 = rows.l10(b);
   if (o0 >= L10) return;
@@ -295,12 +295,12 @@ __device__ unsigned long long g_tob_stamps[kTobStampBlocks][4];
 constexpr int TOB_WAVES = 4;  // 256-thread workgroups (8 waves x 66 KB measured no faster)
 __global__ void __launch_bounds__(64 * TOB_WAVES)
     stoi_tob(const float *__restrict__ y10, int64_t y_ld, int64_t B, Rows rows, const int *__restrict__ idx,
-             const int *__restrict__ kept, int nv_ld, float *__restrict__ tob, int64_t tmax) {
+             const int *__restrict__ kept, int nv_ld, float *__restrict__ tob, int64_t tmax, int64_t b0) {
   __shared__ __attribute__((aligned(16))) float blk[2][TF + 1][128];
   __shared__ __attribute__((aligned(16))) float xbuf[TOB_WAVES * 2 * kFftBuf];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: kept indices by scalar loads
-  const int64_t b = blockIdx.y;
+  const int64_t b = b0 + blockIdx.y;
   const int n = kept[b];
   const int T = n - 2;  // STFT frames of the overlap-added signal: 1 + ((n+1)*128 - 512)/128
   const int64_t L10 = rows.l10(b);
@@ -636,9 +636,11 @@ inline int run_tail(int64_t B, const Geometry &g, const Rows &rows, const float 
                     int *kept, float *tob, int64_t tmax, float *stoi_out, float *estoi_out, hipStream_t st) {
   hipLaunchKernelGGL(stoi_select, dim3((unsigned)B), dim3(256), 0, st, vad, g.v_ld, g.nv_ld, rows, idx, kept);
   FSEM_CHECK_LAUNCH();
-  hipLaunchKernelGGL(stoi_tob, dim3((unsigned)((g.tmax + TF - 1) / TF), (unsigned)B), dim3(64 * TOB_WAVES), 0, st, y10,
-                     g.y_ld, B, rows, idx, kept, g.nv_ld, tob, tmax);
-  FSEM_CHECK_LAUNCH();
+  for (int64_t b0 = 0; b0 < B; b0 += kMaxGridY) {
+    hipLaunchKernelGGL(stoi_tob, dim3((unsigned)((g.tmax + TF - 1) / TF), (unsigned)std::min(B - b0, kMaxGridY)),
+                       dim3(64 * TOB_WAVES), 0, st, y10, g.y_ld, B, rows, idx, kept, g.nv_ld, tob, tmax, b0);
+    FSEM_CHECK_LAUNCH();
+  }
   if (stoi_out) {
     hipLaunchKernelGGL(stoi_seg, dim3((unsigned)B), dim3(SEG_T), 0, st, tob, B, tmax, kept, stoi_out,
                        estoi_out);
@@ -664,7 +666,6 @@ inline int run(const float *ref, const float *deg, int64_t B, int64_t length, in
   if (g.NV <= 0 && !lengths) return FSEM_ESHORT;  // with lengths: NaN rows instead
   const Rows rows{lengths, length, rk.orig, rk.nw};
   if (!ws || ws_size < ws_bytes(B, g)) return FSEM_EWORKSPACE;
-  if (B > 65535) return FSEM_EINVAL;
   Ws w = carve(ws, B, g);
   int64_t tmax = g.tmax;
   if (tob_out) {
@@ -686,11 +687,18 @@ inline int run(const float *ref, const float *deg, int64_t B, int64_t length, in
     if (rc != FSEM_OK) return rc;
     rc = launch_resample_tiled(deg, B, length, ld, lengths, w.y10 + g.y_ld, 2 * g.y_ld, 0, rk, st);
     if (rc != FSEM_OK) return rc;
-    hipLaunchKernelGGL(stoi_vad10, dim3((unsigned)((g.L10 + VQ - 1) / VQ), (unsigned)B), dim3(256), 0, st, w.y10,
-                       g.y_ld, rows, w.vad, g.v_ld);
+    for (int64_t b0 = 0; b0 < B; b0 += kMaxGridY) {
+      hipLaunchKernelGGL(stoi_vad10, dim3((unsigned)((g.L10 + VQ - 1) / VQ), (unsigned)std::min(B - b0, kMaxGridY)),
+                         dim3(256), 0, st, w.y10, g.y_ld, rows, w.vad, g.v_ld, b0);
+      FSEM_CHECK_LAUNCH();
+    }
   } else {
-    hipLaunchKernelGGL(stoi_resample_vad, dim3((unsigned)((g.L10 + VF3 * 128 - 1) / (VF3 * 128)), (unsigned)B),
-                       dim3(256), 0, st, ref, deg, rows, ld, g.mode, rk, w.y10, g.y_ld, w.vad, g.v_ld);
+    for (int64_t b0 = 0; b0 < B; b0 += kMaxGridY) {
+      hipLaunchKernelGGL(stoi_resample_vad,
+                         dim3((unsigned)((g.L10 + VF3 * 128 - 1) / (VF3 * 128)), (unsigned)std::min(B - b0, kMaxGridY)),
+                         dim3(256), 0, st, ref, deg, rows, ld, g.mode, rk, w.y10, g.y_ld, w.vad, g.v_ld, b0);
+      FSEM_CHECK_LAUNCH();
+    }
   }
   FSEM_CHECK_LAUNCH();
   return run_tail(B, g, rows, w.y10, w.vad, w.idx, w.kept, w.tob, tmax, stoi_out, estoi_out, st);
@@ -738,7 +746,6 @@ extern "C" int fsem_pesq_stoi_f32(const float *ref, const float *deg, int64_t ba
                                   size_t ws_bytes, void *stream) {
   if (!ref || !deg || !mos || !stoi_out || !estoi_out || batch <= 0 || length <= 0 || ld < length)
     return FSEM_EINVAL;
-  if (batch > 65535) return FSEM_EINVAL;
   stoi::Geometry g;
   ResampleKernel rk;
   int rc = stoi::make_geometry(length, 16000, &g, &rk);

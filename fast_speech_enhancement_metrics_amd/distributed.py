@@ -35,16 +35,45 @@ def gather_scores(local: torch.Tensor, batch: int, group=None) -> torch.Tensor:
     return torch.cat(rows, 0)
 
 
-def sharded_scores(metric, clean: torch.Tensor, noisy: torch.Tensor, group=None, **kw) -> torch.Tensor:
+def score_columns(metric) -> int:
+    """Columns of ``metric.scores``: 3 (PESQ_STOI: mos, stoi, estoi), 2 (STOI: stoi, estoi), 1 (PESQ)."""
+    from .joint import PESQ_STOI
+    from .STOI import STOI
+    return 3 if isinstance(metric, PESQ_STOI) else (2 if isinstance(metric, STOI) else 1)
+
+
+def collective_device(group, fallback) -> torch.device:
+    """Where the all-gather's tensors must live: the current HIP device for RCCL ("nccl"),
+    else the caller's device (gloo: CPU)."""
+    if dist.get_backend(group) == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device(fallback) if fallback is not None else torch.device("cpu")
+
+
+def _local_scores(metric, clean, noisy, lengths, device) -> torch.Tensor:
+    """[n, k] float32 scores of this rank's rows (rows at metric.sample_rate), n may be 0."""
+    k = score_columns(metric)
+    if noisy is None or noisy.shape[0] == 0:
+        return torch.zeros(0, k, dtype=torch.float32, device=device)
+    res = metric.scores(clean, noisy, lengths=lengths, sample_rate=metric.sample_rate)
+    cols = res if isinstance(res, tuple) else (res,)
+    return torch.stack([c.to(torch.float32) for c in cols], dim=1).to(device)
+
+
+def sharded_scores(metric, clean: torch.Tensor, noisy: torch.Tensor, group=None, lengths=None) -> torch.Tensor:
     """Score the full batch [B, L] data-parallel: this rank computes its shard with
-    ``metric.scores`` and the results are all-gathered -> [B, k] on every rank."""
+    ``metric.scores`` and the results are all-gathered -> [B, k] on every rank.
+
+    Rows are at the metric's configured rate (``metric.sample_rate``; PESQ resamples them to
+    16 kHz, STOI to 10 kHz, as the reference's BaseMetric does); ``lengths`` optionally gives
+    per-row lengths.  A rank whose shard is empty (B < world size) contributes no rows."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     B = clean.shape[0]
     lo, hi = shard_bounds(B, world, rank)
-    res = metric.scores(clean[lo:hi], noisy[lo:hi], **kw)
-    cols = res if isinstance(res, tuple) else (res,)
-    local = torch.stack([c.to(torch.float32) for c in cols], dim=1)
+    lens = None if lengths is None else torch.as_tensor(lengths).reshape(-1)[lo:hi]
+    dev = collective_device(group, noisy.device)
+    local = _local_scores(metric, clean[lo:hi], noisy[lo:hi], lens, dev)
     return gather_scores(local, B, group)
 
 
@@ -64,39 +93,36 @@ def lpt_shards(lengths, world: int) -> list[list[int]]:
 
 
 def sharded_scores_ragged(metric, clean, noisy, group=None, device=None) -> torch.Tensor:
-    """Score a ragged batch (lists of 1-D utterances) data-parallel with LPT balancing by total
-    length: this rank scores its utterances as one padded batch with per-row lengths
-    (``metric.scores(..., lengths=...)``), then the [n_r, k] score rows are all-gathered and put
-    back in the caller's order -> [B, k] on every rank."""
+    """Score a ragged batch (lists of 1-D utterances at ``metric.sample_rate``) data-parallel with
+    LPT balancing by total length: this rank scores its utterances as one padded batch with
+    per-row lengths (``metric.scores(..., lengths=...)``), then the [n_r, k] score rows are
+    all-gathered and put back in the caller's order -> [B, k] on every rank.  ``device``: where
+    this rank computes (default: where the utterances are)."""
     from .batching import pad_batch
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     lengths = [int(x.numel()) for x in noisy]
     plan = lpt_shards(lengths, world)
     mine = plan[rank]
-    c, n, lens = pad_batch([clean[i] for i in mine], [noisy[i] for i in mine]) if mine else (None, None, None)
-    if device is not None and c is not None:
-        c, n = c.to(device), n.to(device)
+    coll = collective_device(group, device if device is not None else (noisy[0].device if noisy else None))
     if mine:
-        # STOI.scores takes the input rate (its resampler is fused); PESQ / PESQ_STOI take 16 kHz rows
-        kw = {"sample_rate": metric.sample_rate} if hasattr(metric, "N") else {}
-        res = metric.scores(c, n, lengths=lens, **kw)
-        cols = res if isinstance(res, tuple) else (res,)
-        local = torch.stack([x.to(torch.float32) for x in cols], dim=1)
-    else:
-        k = 3 if metric.__class__.__name__ == "PESQ_STOI" else (2 if hasattr(metric, "N") else 1)
-        local = torch.zeros(0, k, dtype=torch.float32, device=device or "cpu")
+        c, n, lens = pad_batch([clean[i] for i in mine], [noisy[i] for i in mine])
+        if device is not None:
+            c, n = c.to(device), n.to(device)
+        local = _local_scores(metric, c, n, lens, coll)
+    else:  # empty shard: no rows, but the collective still runs on the right device
+        local = _local_scores(metric, None, None, None, coll)
     cap = max(len(s) for s in plan)
     k = local.shape[1]
-    buf = torch.full((cap, k), float("nan"), dtype=torch.float32, device=local.device)
+    buf = torch.full((cap, k), float("nan"), dtype=torch.float32, device=coll)
     buf[:local.shape[0]] = local
-    out = torch.empty(world * cap, k, dtype=torch.float32, device=local.device)
+    out = torch.empty(world * cap, k, dtype=torch.float32, device=coll)
     if dist.get_backend(group) == "nccl":
         dist.all_gather_into_tensor(out, buf, group=group)
     else:
         dist.all_gather(list(out.chunk(world)), buf, group=group)
-    full = torch.empty(len(lengths), k, dtype=torch.float32, device=local.device)
+    full = torch.empty(len(lengths), k, dtype=torch.float32, device=coll)
     for r, idx in enumerate(plan):
         if idx:
-            full[torch.tensor(idx, device=local.device)] = out[r * cap:r * cap + len(idx)]
+            full[torch.tensor(idx, device=coll)] = out[r * cap:r * cap + len(idx)]
     return full

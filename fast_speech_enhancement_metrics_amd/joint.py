@@ -18,7 +18,7 @@ import torch
 from . import _native
 from .PESQ import PESQ
 from .STOI import STOI
-from .base import BaseMetric, as_rows, device_lengths
+from .base import BaseMetric, as_rows, check_row_rate, device_lengths
 
 
 class PESQ_STOI(BaseMetric):
@@ -43,17 +43,26 @@ class PESQ_STOI(BaseMetric):
                 s = [{"STOI": float("nan"), "ESTOI": float("nan")}] * len(p)
         return [{**a, **b} for a, b in zip(p, s)]
 
-    def scores(self, clean_speech: torch.Tensor, denoised_speech: torch.Tensor, lengths=None):
-        """(mos[B], stoi[B], estoi[B]) on the metric's device, 16 kHz rows (no host sync on GPU)."""
-        if self.sample_rate != self.EXPECTED_SAMPLING_RATE:
-            raise ValueError("PESQ_STOI.scores takes 16 kHz rows; call the metric for other rates")
+    def scores(self, clean_speech: torch.Tensor, denoised_speech: torch.Tensor, lengths=None,
+               sample_rate: int | None = None):
+        """(mos[B], stoi[B], estoi[B]) on the metric's device (no host sync on GPU).
+
+        Rows at ``sample_rate`` (None: 16 kHz, which requires a 16 kHz metric).  16 kHz rows take the
+        fused single-read engine; other rates keep the reference's own resampling paths (PESQ:
+        sr -> 16 kHz, STOI: sr -> 10 kHz directly) through the two engines.
+        """
+        sr = check_row_rate(self, sample_rate)
+        if sr != self.EXPECTED_SAMPLING_RATE:
+            mos = self._pesq.scores(clean_speech, denoised_speech, lengths, sample_rate=sr)
+            s, e = self._stoi.scores(clean_speech, denoised_speech, sr, lengths=lengths)
+            return mos, s, e
         clean = as_rows(clean_speech)
         noisy = as_rows(denoised_speech)
         if noisy.shape != clean.shape:
             raise Exception("`clean_speech` and `denoised_speech` should have the same shape.")
         B, L = clean.shape
         if not clean.is_cuda:
-            mos = self._pesq.scores(clean, noisy, lengths)
+            mos = self._pesq.scores(clean, noisy, lengths, sample_rate=16000)
             s, e = self._stoi.scores(clean, noisy, 16000, lengths=lengths)
             return mos, s, e
         lib = _native.load()
@@ -78,7 +87,7 @@ class PESQ_STOI(BaseMetric):
                        lengths=None) -> list[dict[str, float]]:
         assert clean_speech is not None
         with torch.inference_mode():
-            mos, s, e = (t.float() for t in self.scores(clean_speech, denoised_speech, lengths))
+            mos, s, e = (t.float() for t in self.scores(clean_speech, denoised_speech, lengths, sample_rate=16000))
             m, s, e = torch.stack([mos, s, e]).tolist()
         if all(x != x for x in s):  # as STOI (STOI.py:162-165)
             warnings.warn("Not enough non-silent frames. Please check your sound files", RuntimeWarning, stacklevel=3)

@@ -41,7 +41,7 @@ extern "C" {
 #define FSEM_EWORKSPACE -2    /* workspace smaller than *_workspace_bytes()        */
 #define FSEM_ELAUNCH -3       /* HIP launch / runtime error                        */
 #define FSEM_ESHORT -4        /* input too short for the metric (see each entry)  */
-#define FSEM_ERATE -5         /* unsupported sample-rate pair                      */
+#define FSEM_ERATE -5         /* unsupported sample-rate pair (see resampling)      */
 
 const char *fsem_strerror(int code);
 int fsem_version(void);
@@ -50,6 +50,11 @@ int fsem_version(void);
  * torchaudio.transforms.Resample(orig, new) (sinc_interp_hann, width 6,
  * rolloff 0.99) as used by BaseMetric.prepare_audio   fast_se_metrics/base.py:13,19-20
  * out: [rows, fsem_resample_length(n_in, orig, new)] with row stride ld_out.
+ * Any rate pair whose filter has at most 8192 taps (taps = 2 * ceil(6 * o / (0.99 * min(o, n))) + o
+ * for the reduced pair o -> n = orig / g -> new / g): every common audio rate (8, 11.025, 16,
+ * 22.05, 24, 32, 44.1, 48, 88.2, 96 kHz) to 16 or 10 kHz.  Longer filters (e.g. 44100 -> 16001)
+ * give FSEM_ERATE here and in every entry that resamples (fsem_resample_length returns -1).
+ * rows: any count (launches are sliced internally; no grid-dimension limit reaches the caller).
  */
 int64_t fsem_resample_length(int64_t n_in, int32_t orig_freq, int32_t new_freq);
 int fsem_resample_f32(const float *in, int64_t rows, int64_t n_in, int64_t ld_in,

@@ -20,8 +20,7 @@ def _worker(rank, world, port, out_q):
         g = load_golden("pesq_wide")
         p = sharded_scores(PESQ(16000), torch.from_numpy(g["clean_f"]), torch.from_numpy(g["noisy_f"]))
         gs = load_golden("stoi_wide")
-        s = sharded_scores(STOI(16000), torch.from_numpy(gs["clean_f"]), torch.from_numpy(gs["noisy_f"]),
-                           sample_rate=16000)
+        s = sharded_scores(STOI(16000), torch.from_numpy(gs["clean_f"]), torch.from_numpy(gs["noisy_f"]))
         out_q.put((rank, p.numpy(), s.numpy()))
     finally:
         dist.destroy_process_group()
@@ -114,3 +113,94 @@ def test_lpt_shards_balance():
     loads = [int(lens[s].sum()) for s in plan]
     assert max(loads) - min(loads) <= lens.max()  # LPT bound
     assert (max(loads) - min(loads)) / np.mean(loads) < 0.01
+
+
+def _spawn(target, world, *args):
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+def _worker_rates(rank, world, port, out_q):
+    """Metrics configured for 8 kHz score 8 kHz rows: the helpers pass metric.sample_rate."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from fast_speech_enhancement_metrics_amd import PESQ, PESQ_STOI, STOI
+        from fast_speech_enhancement_metrics_amd.distributed import sharded_scores, sharded_scores_ragged
+        from tests.conftest import load_golden
+        g = load_golden("rate_8k")
+        c, n = torch.from_numpy(g["clean_f"]), torch.from_numpy(g["noisy_f"])
+        p = sharded_scores(PESQ(8000), c, n)
+        s = sharded_scores(STOI(8000), c, n)
+        j = sharded_scores(PESQ_STOI(8000), c, n)
+        pr = sharded_scores_ragged(PESQ(8000), list(c), list(n))
+        out_q.put((rank, p.numpy(), s.numpy(), j.numpy(), pr.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_scores_use_metric_rate():
+    """PESQ(8000) / STOI(8000) / PESQ_STOI(8000) over 2 gloo ranks == the reference's 8 kHz golden
+    (before, scores() treated the 8 kHz rows as 16 kHz / 10 kHz rows)."""
+    from tests.conftest import load_golden
+    g = load_golden("rate_8k")
+    for rank, p, s, j, pr in _spawn(_worker_rates, 2):
+        np.testing.assert_allclose(p[:, 0], g["pesq"], atol=2e-3, rtol=0)
+        np.testing.assert_allclose(pr[:, 0], g["pesq"], atol=2e-3, rtol=0)
+        np.testing.assert_allclose(s[:, 0], g["stoi"], atol=1e-4, rtol=0)
+        np.testing.assert_allclose(s[:, 1], g["estoi"], atol=1e-4, rtol=0)
+        np.testing.assert_allclose(j, np.stack([g["pesq"], g["stoi"], g["estoi"]], 1), atol=2e-3, rtol=0)
+
+
+def test_scores_without_rate_refuse_other_rates():
+    from fast_speech_enhancement_metrics_amd import PESQ, PESQ_STOI, STOI
+    x = torch.zeros(1, 16000)
+    for m in (PESQ(8000), STOI(16000), PESQ_STOI(8000)):
+        with pytest.raises(ValueError, match="sample_rate"):
+            m.scores(x, x)
+
+
+def _worker_empty(rank, world, port, out_q):
+    """Batches smaller than the world: ranks with no rows still join the all-gather."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from fast_speech_enhancement_metrics_amd import PESQ, STOI
+        from fast_speech_enhancement_metrics_amd.distributed import sharded_scores, sharded_scores_ragged
+        from tests.conftest import load_golden
+        g = load_golden("pesq_wide")
+        c, n = torch.from_numpy(g["clean_f"][:1]), torch.from_numpy(g["noisy_f"][:1])
+        p = sharded_scores(PESQ(16000), c, n)
+        s = sharded_scores(STOI(16000), c, n)
+        pr = sharded_scores_ragged(PESQ(16000), list(c), list(n))
+        out_q.put((rank, p.numpy(), s.numpy(), pr.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_empty_shards():
+    from fast_speech_enhancement_metrics_amd import PESQ, STOI
+    from tests.conftest import load_golden
+    g = load_golden("pesq_wide")
+    c, n = torch.from_numpy(g["clean_f"][:1]), torch.from_numpy(g["noisy_f"][:1])
+    ref_p = PESQ(16000).scores(c, n).numpy()
+    ref_s = torch.stack(STOI(16000).scores(c, n, sample_rate=16000), 1).numpy()
+    for rank, p, s, pr in _spawn(_worker_empty, 3):
+        assert p.shape == (1, 1) and s.shape == (1, 2) and pr.shape == (1, 1)
+        np.testing.assert_allclose(p[:, 0], ref_p, atol=1e-6, rtol=0)
+        np.testing.assert_allclose(pr[:, 0], ref_p, atol=1e-6, rtol=0)
+        np.testing.assert_allclose(s, ref_s, atol=1e-6, rtol=0)
