@@ -100,6 +100,11 @@ __device__ __forceinline__ void lds_stores_done() { asm volatile("s_waitcnt lgkm
 
 static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// Longest row any entry accepts (input samples, and 10 / 16 kHz samples after resampling): the
+// kernels address a row with 32-bit byte offsets (raw buffer loads, range-checked descriptors).
+// 2^29 samples = 9.3 h at 16 kHz; longer rows give FSEM_EINVAL (include/fsem.h).
+constexpr int64_t kMaxLength = int64_t(1) << 29;
+
 // Launches that map rows (utterances) to grid.y cover at most kMaxGridY rows each; the host loops
 // over slices [r0, r0 + kMaxGridY) and passes r0 (HIP's grid.y limit, hipDeviceProp maxGridSize[1]).
 constexpr int64_t kMaxGridY = 65535;

@@ -1063,7 +1063,8 @@ extern "C" size_t fsem_pesq_workspace_bytes(int64_t batch, int64_t length) {
 int fsem::pesq::launch_front(const float *ref, const float *deg, int64_t batch, int64_t length, int64_t ld,
                              const int32_t *lengths, float *bark, float *power, void *ws, size_t ws_bytes,
                              float *y10, int64_t y_ld, float2 *vad, int64_t v_ld, hipStream_t st) {
-  if (!ref || !deg || !bark || !power || batch <= 0 || length <= 0 || ld < length) return FSEM_EINVAL;
+  if (!ref || !deg || !bark || !power || batch <= 0 || length <= 0 || ld < length || length > kMaxLength)
+    return FSEM_EINVAL;
   const pesq::Geometry g = pesq::geometry(length);
   if (g.F < 20 && !lengths) return FSEM_ESHORT;
   if (ws_bytes < fsem_pesq_front_workspace_bytes(batch, length) || !ws) return FSEM_EWORKSPACE;
@@ -1121,7 +1122,7 @@ extern "C" size_t fsem_pesq_back_workspace_bytes(int64_t batch, int64_t length) 
 extern "C" int fsem_pesq_back_f32(const float *bark, const float *power, int64_t batch, int64_t length,
                                   const int32_t *lengths, float *mos, void *ws, size_t ws_bytes,
                                   void *stream) {
-  if (!bark || !power || !mos || batch <= 0 || length <= 0) return FSEM_EINVAL;
+  if (!bark || !power || !mos || batch <= 0 || length <= 0 || length > kMaxLength) return FSEM_EINVAL;
   const pesq::Geometry g = pesq::geometry(length);
   if (g.F < 20 && !lengths) return FSEM_ESHORT;
   if (!ws || ws_bytes < fsem_pesq_back_workspace_bytes(batch, length)) return FSEM_EWORKSPACE;
@@ -1181,7 +1182,7 @@ static WbWs carve_wb(void *ws, int64_t batch, int64_t length) {
 int fsem::pesq::run_wb_front(const float *ref, const float *deg, int64_t batch, int64_t length, int64_t ld,
                              const int32_t *lengths, void *ws, size_t ws_bytes, float *y10, int64_t y_ld,
                              float2 *vad, int64_t v_ld, hipStream_t stream) {
-  if (!ref || !deg || batch <= 0 || length <= 0 || ld < length) return FSEM_EINVAL;
+  if (!ref || !deg || batch <= 0 || length <= 0 || ld < length || length > kMaxLength) return FSEM_EINVAL;
   const pesq::Geometry g = pesq::geometry(length);
   if (g.F < 20 && !lengths) return FSEM_ESHORT;
   if (!ws || ws_bytes < fsem_pesq_workspace_bytes(batch, length)) return FSEM_EWORKSPACE;

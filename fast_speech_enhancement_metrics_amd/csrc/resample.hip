@@ -364,26 +364,26 @@ extern "C" int64_t fsem_resample_length(int64_t n_in, int32_t orig_freq, int32_t
 extern "C" int fsem_resample_f32(const float *in, int64_t rows, int64_t n_in, int64_t ld_in,
                                  float *out, int64_t ld_out, int32_t orig_freq, int32_t new_freq,
                                  void *stream) {
-  if (!in || !out || rows < 0 || n_in < 0 || ld_in < n_in) return FSEM_EINVAL;
+  if (!in || !out || rows < 0 || n_in < 0 || ld_in < n_in || n_in > fsem::kMaxLength) return FSEM_EINVAL;
   if (rows == 0 || n_in == 0) return FSEM_OK;
   fsem::ResampleKernel rk;
   int rc = fsem::make_resample_kernel(orig_freq, new_freq, &rk);
   if (rc != FSEM_OK) return rc;
   const int64_t n_out = (rk.nw * n_in + rk.orig - 1) / rk.orig;
-  if (ld_out < n_out) return FSEM_EINVAL;
+  if (ld_out < n_out || n_out > fsem::kMaxLength) return FSEM_EINVAL;
   return fsem::launch_resample_tiled(in, rows, n_in, ld_in, nullptr, out, ld_out, 0, rk, (hipStream_t)stream);
 }
 
 extern "C" int fsem_resample_rows_f32(const float *in, int64_t rows, int64_t n_in, int64_t ld_in,
                                       const int32_t *lengths, float *out, int64_t ld_out, int32_t orig_freq,
                                       int32_t new_freq, void *stream) {
-  if (!in || !out || !lengths || rows < 0 || n_in < 0 || ld_in < n_in) return FSEM_EINVAL;
+  if (!in || !out || !lengths || rows < 0 || n_in < 0 || ld_in < n_in || n_in > fsem::kMaxLength) return FSEM_EINVAL;
   if (orig_freq == new_freq) return FSEM_ERATE;  // nothing to resample: the caller keeps its rows
   if (rows == 0 || n_in == 0) return FSEM_OK;
   fsem::ResampleKernel rk;
   int rc = fsem::make_resample_kernel(orig_freq, new_freq, &rk);
   if (rc != FSEM_OK) return rc;
   const int64_t n_out = (rk.nw * n_in + rk.orig - 1) / rk.orig;
-  if (ld_out < n_out) return FSEM_EINVAL;
+  if (ld_out < n_out || n_out > fsem::kMaxLength) return FSEM_EINVAL;
   return fsem::launch_resample_tiled(in, rows, n_in, ld_in, lengths, out, ld_out, n_out, rk, (hipStream_t)stream);
 }

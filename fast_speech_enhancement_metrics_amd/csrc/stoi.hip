@@ -719,7 +719,8 @@ extern "C" size_t fsem_stoi_workspace_bytes(int64_t batch, int64_t length, int32
 extern "C" int fsem_stoi_f32(const float *ref, const float *deg, int64_t batch, int64_t length, int64_t ld,
                              const int32_t *lengths, int32_t sample_rate, float *stoi_out, float *estoi_out,
                              void *ws, size_t ws_bytes, void *stream) {
-  if (!ref || !deg || !stoi_out || !estoi_out || batch <= 0 || length <= 0 || ld < length) return FSEM_EINVAL;
+  if (!ref || !deg || !stoi_out || !estoi_out || batch <= 0 || length <= 0 || ld < length || length > kMaxLength)
+    return FSEM_EINVAL;
   return stoi::run(ref, deg, batch, length, ld, lengths, sample_rate, stoi_out, estoi_out, nullptr, nullptr, 0,
                    ws, ws_bytes, (hipStream_t)stream);
 }
@@ -727,7 +728,8 @@ extern "C" int fsem_stoi_f32(const float *ref, const float *deg, int64_t batch, 
 extern "C" int fsem_stoi_tob_f32(const float *ref10, const float *deg10, int64_t batch, int64_t length10,
                                  int64_t ld, int32_t *kept, float *tob, int64_t tmax, void *ws, size_t ws_bytes,
                                  void *stream) {
-  if (!ref10 || !deg10 || !kept || !tob || batch <= 0 || length10 <= 0 || ld < length10) return FSEM_EINVAL;
+  if (!ref10 || !deg10 || !kept || !tob || batch <= 0 || length10 <= 0 || ld < length10 || length10 > kMaxLength)
+    return FSEM_EINVAL;
   stoi::Geometry g;
   ResampleKernel rk;
   int rc = stoi::make_geometry(length10, 10000, &g, &rk);
@@ -744,7 +746,8 @@ extern "C" size_t fsem_pesq_stoi_workspace_bytes(int64_t batch, int64_t length) 
 extern "C" int fsem_pesq_stoi_f32(const float *ref, const float *deg, int64_t batch, int64_t length, int64_t ld,
                                   const int32_t *lengths, float *mos, float *stoi_out, float *estoi_out, void *ws,
                                   size_t ws_bytes, void *stream) {
-  if (!ref || !deg || !mos || !stoi_out || !estoi_out || batch <= 0 || length <= 0 || ld < length)
+  if (!ref || !deg || !mos || !stoi_out || !estoi_out || batch <= 0 || length <= 0 || ld < length ||
+      length > kMaxLength)
     return FSEM_EINVAL;
   stoi::Geometry g;
   ResampleKernel rk;

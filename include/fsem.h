@@ -23,6 +23,8 @@
  *    is then the row capacity, sizing workspace and layouts) and its result is that of the
  *    reference called on the unpadded row alone; rows too short for the metric give NaN
  *    (instead of FSEM_ESHORT, which only the whole-batch form returns);
+ *  - rows are at most 2^29 samples long (9.3 h at 16 kHz), before and after any resampling:
+ *    the kernels address rows with 32-bit byte offsets; longer rows give FSEM_EINVAL;
  *  - return 0 on success or a negative FSEM_E* code (fsem_strerror() for text);
  *  - re-entrant across streams / devices (launches use the current HIP device).
  */

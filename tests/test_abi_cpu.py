@@ -62,6 +62,14 @@ def test_invalid_arguments_are_rejected_without_launch(lib):
     assert lib.fsem_pesq_wb_f32(p, p, 4, 160000, 160000, null, p, p, 16, null) == -2
     assert lib.fsem_stoi_f32(p, p, 4, 160000, 160000, null, 16000, p, p, p, 16, null) == -2
     assert lib.fsem_stoi_workspace_bytes(4, 160000, 16000) > 0
+    # rows past 2^29 samples (32-bit byte offsets in the kernels): rejected before any launch
+    big = (1 << 29) + 4
+    assert lib.fsem_pesq_wb_f32(p, p, 1, big, big, null, p, p, 1 << 62, null) == -1
+    assert lib.fsem_stoi_f32(p, p, 1, big, big, null, 16000, p, p, p, 1 << 62, null) == -1
+    assert lib.fsem_pesq_stoi_f32(p, p, 1, big, big, null, p, p, p, p, 1 << 62, null) == -1
+    assert lib.fsem_resample_f32(p, 1, big, big, p, big, 16000, 10000, null) == -1
+    n = (1 << 28) + 1  # 8 -> 16 kHz: 2^29 + 2 output samples
+    assert lib.fsem_resample_f32(p, 1, n, n, p, 1 << 30, 8000, 16000, null) == -1
     assert lib.fsem_pesq_workspace_bytes(4096, 160000) > 4096 * 2 * 624 * 49 * 4
 
 
