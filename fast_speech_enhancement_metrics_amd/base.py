@@ -7,6 +7,7 @@ own CPU implementation (``_cpu.py``), the reference's CPU mode.
 """
 from __future__ import annotations
 
+import functools
 from abc import ABC, abstractmethod
 
 import torch
@@ -121,13 +122,18 @@ def check_row_rate(metric, sample_rate: int | None) -> int:
     return int(sample_rate)
 
 
+@functools.lru_cache(maxsize=32)
+def _resampler(orig: int, new: int) -> Resample:
+    # one module per rate pair, kept on the host: its CUDA path runs in libfsem and never reads the
+    # kernel buffer, so no per-call host -> device copy (which would wait for the stream to drain)
+    return Resample(orig, new)
+
+
 def resample_rows(clean, noisy, lengths, orig: int, new: int):
     """(clean, noisy, lengths) resampled orig -> new, each row as the row alone when ``lengths`` is
     given (BaseMetric.prepare_audio, base.py:19-20); lengths become the resampled lengths."""
-    rs = Resample(orig, new)
+    rs = _resampler(int(orig), int(new))
     noisy = torch.atleast_2d(noisy)
-    if noisy.is_cuda:
-        rs = rs.to(noisy.device)
     lens = None
     if lengths is not None:
         lens = device_lengths(lengths, noisy.shape[0], noisy.shape[-1], noisy.device)
