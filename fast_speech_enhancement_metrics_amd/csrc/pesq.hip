@@ -842,20 +842,24 @@ __device__ __forceinline__ float loud(float p, int b) {
   return (p > kThresh[b]) ? v : 0.f;
 }
 
-// One wave per utterance, lane = frame: each load brings one band of 64 consecutive frames
+// BW waves per utterance, lane = frame: each load brings one band of 64 consecutive frames
 // (band-major rows, bark_ld), straight into registers -- no LDS staging, so occupancy is set
 // by VGPRs alone (the frame's 49 clean and 49 denoised band values stay in registers per chunk).
-constexpr int BT = 64;
-
-__global__ void __launch_bounds__(BT) __attribute__((amdgpu_waves_per_eu(4)))
+// The utterance's chunks are dealt round-robin to its waves.  BW = 1 for batches that fill the
+// chip (no barriers, no idle waves at the end of an utterance: the throughput form); BW = 4 for
+// small batches, where one utterance's latency is the call's.  The two differ only in the
+// summation order of the band totals and of the window L2 sum (~1e-7 relative in the score).
+template <int BW>
+__global__ void __launch_bounds__(64 * BW) __attribute__((amdgpu_waves_per_eu(4)))
     pesq_back(const float *__restrict__ bark, const float *__restrict__ power, int64_t B, int64_t Lcap,
               const int32_t *__restrict__ lens, int Fcap, float *__restrict__ scratch, float *__restrict__ mos) {
-  const int lane = threadIdx.x;
+  constexpr int BT = 64 * BW;
+  const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t b = blockIdx.x;
   const int64_t L = row_length(lens, b, Lcap);
   const int F = frames_of(L);  // this utterance's frames; rows are laid out with stride bark_ld(Fcap)
   if (F < 20) {  // the reference's unfold(1, 20, 10) raises here (PESQ.py:169)
-    if (lane == 0) mos[b] = __builtin_nanf("");
+    if (tid == 0) mos[b] = __builtin_nanf("");
     return;
   }
   const int64_t fld = bark_ld(Fcap);
@@ -875,25 +879,32 @@ __global__ void __launch_bounds__(BT) __attribute__((amdgpu_waves_per_eu(4)))
   auto ld = [](__amdgpu_buffer_rsrc_t r, int voff, int soff) {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
   };
-  // scratch row of this utterance: [sym | asym] per frame (stride 4 * Fcap, two slots unused)
+  // scratch row of this utterance (stride 4 * Fcap): sym [0, F), asym [F, 2F), and with several
+  // waves the keep flags from 2 Fcap on (one word per frame, written and read back by one lane)
   float *__restrict__ sym = scratch + b * (int64_t)Fcap * 4;
   float *__restrict__ asym = sym + F;
+  int *__restrict__ keepf = reinterpret_cast<int *>(sym + 2 * (int64_t)Fcap);
   // PESQ.py:97-100 -- power = sum / (L + 5120) / 1.04684; bark scales by 1e7 / power
   const float pc = power[b] / (float)(L + 5120) / 1.04684f;
   const float pn = power[b + B] / (float)(L + 5120) / 1.04684f;
   const float sc = 1e7f / pc, sn = 1e7f / pn;
+  const int nch = (F + 63) / 64;
 
   // ---- pass 1: silent frames (PESQ.py:146, loudness.py:48-53 x 1e2) and per-lane partial band
   // sums of the audible power of non-silent frames (loudness.py:55-60).  The clean sweep keeps
-  // each chunk's keep flags as a ballot (LDS), so the denoised sums follow in a second sweep
-  // without the clean accumulators live.
-  extern __shared__ unsigned long long keepm[];  // [ceil(Fcap / 64)]
+  // each frame's keep flag, so the denoised sums follow in a second sweep without the clean
+  // accumulators live: one wave keeps a ballot per chunk in LDS ([ceil(Fcap / 64)], dynamic);
+  // several waves keep a word per frame in the scratch row, each lane reading back its own.
+  extern __shared__ unsigned long long keepm[];
   __shared__ float ratio_s[NBARK];
+  __shared__ float red[BW][16 * 65];
+  __shared__ float tot[2][BW][NBARK];
+  __shared__ double dred[2][BW];
   float acc[NBARK];
 #pragma unroll
   for (int k = 0; k < NBARK; ++k) acc[k] = 0.f;
-  for (int f0 = 0; f0 < F; f0 += BT) {
-    const int f = f0 + lane;
+  for (int c = wv; c < nch; c += BW) {
+    const int f = 64 * c + lane;
     const bool valid = f < F;
     const int fi = valid ? f : F - 1;  // clamped: every load in bounds, results masked
     int fs = fstride;
@@ -902,64 +913,82 @@ __global__ void __launch_bounds__(BT) __attribute__((amdgpu_waves_per_eu(4)))
     float a = 0.f;
 #pragma unroll
     for (int k = 0; k < NBARK; ++k) {
-      const float c = ld(rcl, 4 * fi + k * fs, 0) * sc;
-      aud[k] = (c > kThresh[k] * 100.f) ? c : 0.f;
+      const float cl = ld(rcl, 4 * fi + k * fs, 0) * sc;
+      aud[k] = (cl > kThresh[k] * 100.f) ? cl : 0.f;
       a += aud[k];
     }
     const bool keep = valid && !(a < 1e7f);
-    const unsigned long long km = __ballot(keep);
-    if (lane == 0) keepm[f0 / BT] = km;
+    if (BW == 1) {
+      const unsigned long long km = __ballot(keep);
+      if (lane == 0) keepm[c] = km;
+    } else if (valid) {
+      keepf[f] = keep;
+    }
 #pragma unroll
     for (int k = 0; k < NBARK; ++k) acc[k] += keep ? aud[k] : 0.f;
   }
-  // lane-partial band sums -> totals by an LDS transpose, 16 bands per round (row = band over
-  // the 64 lanes, stride 65: conflict-free both ways); lane k < 49 ends up holding band k's total
-  __shared__ float red[16 * 65];
-  auto band_totals = [&](float v[NBARK]) {
+  // lane-partial band sums -> this wave's totals by an LDS transpose, 16 bands per round (row =
+  // band over the 64 lanes, stride 65: conflict-free both ways); lane k < 49 ends up holding
+  // band k's total over the wave's chunks, which goes to tot[s][wave][k]
+  auto band_totals = [&](float v[NBARK], int s) {
     float t = 0.f;
+    float *rw = red[wv];
 #pragma unroll
     for (int k0 = 0; k0 < NBARK; k0 += 16) {
 #pragma unroll
-      for (int k = k0; k < k0 + 16 && k < NBARK; ++k) red[(k - k0) * 65 + lane] = v[k];
-      __syncthreads();
+      for (int k = k0; k < k0 + 16 && k < NBARK; ++k) rw[(k - k0) * 65 + lane] = v[k];
+      wave_lds_fence();
       if (lane >= k0 && lane < k0 + 16 && lane < NBARK) {
 #pragma unroll 16
-        for (int j = 0; j < 64; ++j) t += red[(lane - k0) * 65 + j];
+        for (int j = 0; j < 64; ++j) t += rw[(lane - k0) * 65 + j];
       }
-      __syncthreads();
+      wave_lds_fence();
     }
-    return t;
+    if (lane < NBARK) tot[s][wv][lane] = t;
   };
-  const float mc_tot = band_totals(acc);
+  band_totals(acc, 0);
+  if (BW > 1) __threadfence_block();  // the keep flags, read back below
 #pragma unroll
   for (int k = 0; k < NBARK; ++k) acc[k] = 0.f;
-  for (int f0 = 0; f0 < F; f0 += BT) {
-    const int f = f0 + lane;
+  for (int c = wv; c < nch; c += BW) {
+    const int f = 64 * c + lane;
     const int fi = f < F ? f : F - 1;
     int fs = fstride;
     asm volatile("" : "+s"(fs));
-    const bool keep = (keepm[f0 / BT] >> lane) & 1ull;
+    const bool keep = (BW == 1) ? ((keepm[c] >> lane) & 1ull) : ((f < F) && keepf[fi]);
 #pragma unroll
     for (int k = 0; k < NBARK; ++k) {
       const float n = ld(rdn, 4 * fi + k * fs, 0) * sn;
       acc[k] += (keep && n > kThresh[k] * 100.f) ? n : 0.f;
     }
   }
-  const float mn_tot = band_totals(acc);
-  // band power ratio (PESQ.py:151-152)
-  if (lane < NBARK) {
-    const float c = mc_tot / (float)F, n = mn_tot / (float)F;
-    ratio_s[lane] = fminf(fmaxf((n + 1000.f) / (c + 1000.f), 0.01f), 100.f);
+  band_totals(acc, 1);
+  lds_barrier();
+  // band power ratio (PESQ.py:151-152), wave totals summed in wave order
+  if (tid < NBARK) {
+    float mc = 0.f, mn = 0.f;
+#pragma unroll
+    for (int w = 0; w < BW; ++w) {
+      mc += tot[0][w][tid];
+      mn += tot[1][w][tid];
+    }
+    const float cm = mc / (float)F, nm = mn / (float)F;
+    ratio_s[tid] = fminf(fmaxf((nm + 1000.f) / (cm + 1000.f), 0.01f), 100.f);
   }
-  __syncthreads();
+  lds_barrier();
 
-  // ---- pass 2: frame ratio (PESQ.py:157-163), loudness, disturbances (PESQ.py:186-224)
+  // ---- pass 2: frame ratio (PESQ.py:157-163), loudness, disturbances (PESQ.py:186-224).
+  // The ratio smoothing reads the previous frame's ratio: one wave carries it from chunk to
+  // chunk; with several waves a chunk is 63 new frames plus, in lane 0, the frame before them
+  // (its ratio only), so the chunks are independent.
+  constexpr int CW = BW == 1 ? 64 : 63, OFF = BW == 1 ? 0 : 1;
   const float sqrt_tw = sqrtf((float)kTotalWidth);
-  float fr_prev = 0.f;  // frame power ratio of the previous chunk's last frame
-  for (int f0 = 0; f0 < F; f0 += BT) {
-    const int f = f0 + lane;
-    const bool valid = f < F;
-    const int fi = valid ? f : F - 1;
+  const int nch2 = (F + CW - 1) / CW;
+  float fr_prev = 0.f;  // BW == 1: ratio of the previous chunk's last frame
+  for (int c = wv; c < nch2; c += BW) {
+    const int f = CW * c - OFF + lane;
+    const bool valid = (OFF == 0 || lane > 0) && f < F;
+    const int fi = f < 0 ? 0 : (f < F ? f : F - 1);
     int fs = fstride;
     asm volatile("" : "+s"(fs));
     float ec[NBARK], ns[NBARK];
@@ -973,8 +1002,10 @@ __global__ void __launch_bounds__(BT) __attribute__((amdgpu_waves_per_eu(4)))
     }
     const float fr = (ac + 5e3f) / (an + 5e3f);
     float prev = __shfl_up(fr, 1, 64);
-    if (lane == 0) prev = fr_prev;
-    fr_prev = __shfl(fr, 63, 64);
+    if (OFF == 0) {
+      if (lane == 0) prev = fr_prev;
+      fr_prev = __shfl(fr, 63, 64);
+    }
     float r = (f >= 1) ? 0.8f * fr + 0.2f * prev : fr;  // non-recursive (PESQ.py:161)
     r = fminf(fmaxf(r, 3e-4f), 5.f);
     float s2 = 0.f, as = 0.f;
@@ -1001,11 +1032,11 @@ __global__ void __launch_bounds__(BT) __attribute__((amdgpu_waves_per_eu(4)))
       asym[f] = fminf(ay / w, 45.f);
     }
   }
-  __syncthreads();  // pass 3 reads other lanes' sym / asym stores
+  __syncthreads();  // pass 3 reads other waves' sym / asym stores
   // ---- pass 3: L6 within 20-frame windows (hop 10), L2 across windows (PESQ.py:168-172)
   const int nw = (F - 20) / 10 + 1;
   double as_ = 0.0, aa_ = 0.0;
-  for (int w = lane; w < nw; w += BT) {
+  for (int w = tid; w < nw; w += BT) {
     double s6 = 0.0, a6 = 0.0;
     for (int i = 0; i < 20; ++i) {
       const double x = sym[10 * w + i], y = asym[10 * w + i];
@@ -1020,7 +1051,18 @@ __global__ void __launch_bounds__(BT) __attribute__((amdgpu_waves_per_eu(4)))
   as_ = wave_sum_d(as_);
   aa_ = wave_sum_d(aa_);
   if (lane == 0) {
-    const double ds = sqrt(as_ / nw), da = sqrt(aa_ / nw);
+    dred[0][wv] = as_;
+    dred[1][wv] = aa_;
+  }
+  lds_barrier();
+  if (tid == 0) {
+    double ts = 0.0, ta = 0.0;
+#pragma unroll
+    for (int w = 0; w < BW; ++w) {
+      ts += dred[0][w];
+      ta += dred[1][w];
+    }
+    const double ds = sqrt(ts / nw), da = sqrt(ta / nw);
     double m = 4.5 - 0.1 * ds - 0.0309 * da;              // PESQ.py:240
     m = 0.999 + 4.0 / (1.0 + exp(-1.3669 * m + 3.8224));  // PESQ.py:243
     // a signal with zero (or non-finite) band-pass power: the reference's x * sqrt(1e7 / power)
@@ -1127,9 +1169,24 @@ extern "C" int fsem_pesq_back_f32(const float *bark, const float *power, int64_t
   if (g.F < 20 && !lengths) return FSEM_ESHORT;
   if (!ws || ws_bytes < fsem_pesq_back_workspace_bytes(batch, length)) return FSEM_EWORKSPACE;
   if (batch > 0x7fffffff) return FSEM_EINVAL;
-  const size_t keep_bytes = sizeof(unsigned long long) * (size_t)((g.F + pesq::BT - 1) / pesq::BT);
-  hipLaunchKernelGGL(pesq::pesq_back, dim3((unsigned)batch), dim3(pesq::BT), keep_bytes, (hipStream_t)stream, bark,
-                     power, batch, length, lengths, g.F, static_cast<float *>(ws), mos);
+  // 4 waves per utterance for batches up to 2 rows per CU (measured: 10 s rows, B = 256 --
+  // 0.083 vs 0.100 ms; from B = 1024 on the one-wave form is as fast or faster, and leaves more
+  // room to the STOI segment kernel beside it in the joint entry); one wave also needs its keep
+  // ballots in LDS.  FSEM_BACK_WAVES (diagnostics only) forces 1 or 4.
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  static const int forced = [] {
+    const char *e = getenv("FSEM_BACK_WAVES");
+    return e ? atoi(e) : 0;
+  }();
+  const size_t keep_bytes = sizeof(unsigned long long) * (size_t)((g.F + 63) / 64);
+  const bool wide = keep_bytes > 32768 || (forced ? forced == 4 : batch <= 2 * (int64_t)ncu);
+  if (wide)
+    hipLaunchKernelGGL(pesq::pesq_back<4>, dim3((unsigned)batch), dim3(256), 0, (hipStream_t)stream, bark, power,
+                       batch, length, lengths, g.F, static_cast<float *>(ws), mos);
+  else
+    hipLaunchKernelGGL(pesq::pesq_back<1>, dim3((unsigned)batch), dim3(64), keep_bytes, (hipStream_t)stream, bark, power,
+                       batch, length, lengths, g.F, static_cast<float *>(ws), mos);
   FSEM_CHECK_LAUNCH();
   return FSEM_OK;
 }

@@ -429,7 +429,9 @@ __global__ void __launch_bounds__(64 * TOB_WAVES)
 }
 
 // One lane per 30-frame segment m: x[j][t] = X[j][m + t], y likewise (STOI.py:121-198).
-// 128-lane workgroups; clean and denoised envelopes interleaved in LDS as (x, y) pairs (19 KB),
+// 128-lane workgroups, one per (utterance, block of 128 segments): grid (B, P), so a short
+// batch still fills the chip; each writes its block's two correlation sums (double) to
+// part[b][p], which stoi_seg_sum adds up in block order (batch-independent); clean and denoised envelopes interleaved in LDS as (x, y) pairs (19 KB),
 // so every clean/denoised pair of operations is one packed-FP32 instruction (v_pk_fma_f32 /
 // v_pk_add_f32 / v_pk_mul_f32: twice the v_fma_f32 rate on gfx950).  The per-lane row
 // statistics of the ESTOI time normalisation stay in registers (uniform-index writes from the
@@ -438,29 +440,24 @@ constexpr int SEG_T = 128;
 typedef float f2 __attribute__((ext_vector_type(2)));
 __global__ void __launch_bounds__(SEG_T, 3)
     stoi_seg(const float *__restrict__ tob, int64_t B, int64_t tmax, const int *__restrict__ kept,
-             float *__restrict__ stoi_out, float *__restrict__ estoi_out) {
+             double *__restrict__ part, int P, int64_t b0) {
   constexpr int W = SEG_T + NSEG;  // frames per pass
   constexpr int LDX = W + 1;
   __shared__ f2 XY[NB][LDX];
   __shared__ double red[4];
   const int tid = threadIdx.x;
-  const int64_t b = blockIdx.x;
+  const int64_t b = b0 + blockIdx.y;
+  const int p = blockIdx.x;
   const int n = kept[b];
   const int S = n - 31;  // num_segments = (len - 512)//128 - 30 + 2 with len = (n+1)*128 (STOI.py:183-186)
-  if (S <= 0) {
-    if (tid == 0) {
-      stoi_out[b] = __builtin_nanf("");
-      estoi_out[b] = __builtin_nanf("");
-    }
-    return;
-  }
+  const int m0 = p * SEG_T;
+  if (m0 >= S) return;  // past this row's segments (stoi_seg_sum reads blocks p < ceil(S / 128))
   const int T = n - 2;
   const float *xc = tob + (b * NB) * tmax;
   const float *xd = tob + ((b + B) * NB) * tmax;
   double st = 0.0, et = 0.0;
   constexpr float kInvN = 1.f / NSEG;
-  for (int m0 = 0; m0 < S; m0 += SEG_T) {
-    lds_barrier();
+  {
     const int nf = min(W, T - m0);
     // all 2 x 15 x 158 loads of the pass in flight at once (one latency round), then the stores
     {
@@ -564,10 +561,37 @@ __global__ void __launch_bounds__(SEG_T, 3)
   }
   lds_barrier();
   if (tid == 0) {
-    stoi_out[b] = (float)((red[0] + red[2]) / NB / S);   // compute_correlation / num_segments (STOI.py:150,198)
-    estoi_out[b] = (float)((red[1] + red[3]) / NSEG / S);
+    part[(b * P + p) * 2] = red[0] + red[2];
+    part[(b * P + p) * 2 + 1] = red[1] + red[3];
   }
 }
+
+// Per-utterance totals of stoi_seg's block sums, in block order: compute_correlation /
+// num_segments (STOI.py:150,198); NaN without a full segment.
+__global__ void __launch_bounds__(256)
+    stoi_seg_sum(const double *__restrict__ part, int P, int64_t B, const int *__restrict__ kept,
+                 float *__restrict__ stoi_out, float *__restrict__ estoi_out) {
+  const int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const int S = kept[b] - 31;
+  if (S <= 0) {
+    stoi_out[b] = __builtin_nanf("");
+    estoi_out[b] = __builtin_nanf("");
+    return;
+  }
+  const int np = (S + SEG_T - 1) / SEG_T;
+  const double *q = part + b * P * 2;
+  double st = 0.0, et = 0.0;
+  for (int p = 0; p < np; ++p) {
+    st += q[2 * p];
+    et += q[2 * p + 1];
+  }
+  stoi_out[b] = (float)(st / NB / S);
+  estoi_out[b] = (float)(et / NSEG / S);
+}
+
+// segment blocks per row of a tob buffer with tmax frames (S <= tmax - 29)
+inline int seg_blocks(int64_t tmax) { return tmax > 29 ? (int)((tmax - 29 + SEG_T - 1) / SEG_T) : 1; }
 
 struct Geometry {
   int64_t L10;
@@ -605,6 +629,7 @@ inline size_t ws_bytes(int64_t B, const Geometry &g) {
   s += align_up(sizeof(int) * (size_t)B * g.nv_ld, 256);                  // kept indices
   s += align_up(sizeof(int) * (size_t)B, 256);                            // kept counts
   s += align_up(sizeof(float) * (size_t)(2 * B) * NB * (size_t)g.tmax, 256);  // tob
+  s += align_up(sizeof(double) * 2 * (size_t)B * (size_t)seg_blocks(g.tmax), 256);  // segment block sums
   s += align_up(sizeof(float) * (size_t)(2 * B) * (size_t)g.y_ld, 256);      // 10 kHz signals
   return s;
 }
@@ -614,6 +639,7 @@ struct Ws {
   float2 *vad;
   int *idx, *kept;
   float *tob, *y10;
+  double *part;
 };
 
 inline Ws carve(void *ws, int64_t B, const Geometry &g) {
@@ -626,14 +652,31 @@ inline Ws carve(void *ws, int64_t B, const Geometry &g) {
   w.kept = reinterpret_cast<int *>(p);
   p += align_up(sizeof(int) * (size_t)B, 256);
   w.tob = reinterpret_cast<float *>(p);
+  p += align_up(sizeof(float) * (size_t)(2 * B) * NB * (size_t)g.tmax, 256);
+  w.part = reinterpret_cast<double *>(p);
   w.y10 = reinterpret_cast<float *>(static_cast<char *>(ws) + ws_bytes(B, g) -
                                     align_up(sizeof(float) * (size_t)(2 * B) * (size_t)g.y_ld, 256));
   return w;
 }
 
 // Everything after the clean frame energies: selection, band envelopes, segments.
+inline int run_seg(int64_t B, const float *tob, int64_t tmax, const int *kept, double *part, float *stoi_out,
+                   float *estoi_out, hipStream_t st) {
+  const int P = seg_blocks(tmax);
+  for (int64_t b0 = 0; b0 < B; b0 += kMaxGridY) {
+    hipLaunchKernelGGL(stoi_seg, dim3((unsigned)P, (unsigned)std::min(B - b0, kMaxGridY)), dim3(SEG_T), 0, st, tob,
+                       B, tmax, kept, part, P, b0);
+    FSEM_CHECK_LAUNCH();
+  }
+  hipLaunchKernelGGL(stoi_seg_sum, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st, part, P, B, kept, stoi_out,
+                     estoi_out);
+  FSEM_CHECK_LAUNCH();
+  return FSEM_OK;
+}
+
 inline int run_tail(int64_t B, const Geometry &g, const Rows &rows, const float *y10, const float2 *vad, int *idx,
-                    int *kept, float *tob, int64_t tmax, float *stoi_out, float *estoi_out, hipStream_t st) {
+                    int *kept, float *tob, int64_t tmax, double *part, float *stoi_out, float *estoi_out,
+                    hipStream_t st) {
   hipLaunchKernelGGL(stoi_select, dim3((unsigned)B), dim3(256), 0, st, vad, g.v_ld, g.nv_ld, rows, idx, kept);
   FSEM_CHECK_LAUNCH();
   for (int64_t b0 = 0; b0 < B; b0 += kMaxGridY) {
@@ -641,18 +684,7 @@ inline int run_tail(int64_t B, const Geometry &g, const Rows &rows, const float 
                        dim3(64 * TOB_WAVES), 0, st, y10, g.y_ld, B, rows, idx, kept, g.nv_ld, tob, tmax, b0);
     FSEM_CHECK_LAUNCH();
   }
-  if (stoi_out) {
-    hipLaunchKernelGGL(stoi_seg, dim3((unsigned)B), dim3(SEG_T), 0, st, tob, B, tmax, kept, stoi_out,
-                       estoi_out);
-    FSEM_CHECK_LAUNCH();
-  }
-  return FSEM_OK;
-}
-
-inline int run_seg(int64_t B, const float *tob, int64_t tmax, const int *kept, float *stoi_out, float *estoi_out,
-                   hipStream_t st) {
-  hipLaunchKernelGGL(stoi_seg, dim3((unsigned)B), dim3(SEG_T), 0, st, tob, B, tmax, kept, stoi_out, estoi_out);
-  FSEM_CHECK_LAUNCH();
+  if (stoi_out) return run_seg(B, tob, tmax, kept, part, stoi_out, estoi_out, st);
   return FSEM_OK;
 }
 
@@ -701,7 +733,7 @@ inline int run(const float *ref, const float *deg, int64_t B, int64_t length, in
     }
   }
   FSEM_CHECK_LAUNCH();
-  return run_tail(B, g, rows, w.y10, w.vad, w.idx, w.kept, w.tob, tmax, stoi_out, estoi_out, st);
+  return run_tail(B, g, rows, w.y10, w.vad, w.idx, w.kept, w.tob, tmax, w.part, stoi_out, estoi_out, st);
 }
 
 }  // namespace stoi
@@ -766,13 +798,13 @@ extern "C" int fsem_pesq_stoi_f32(const float *ref, const float *deg, int64_t ba
   const hipStream_t side = side_stream(st);
   rc = pesq::run_wb_front(ref, deg, batch, length, ld, lengths, ws, pesq_bytes, w.y10, g.y_ld, w.vad, g.v_ld, st);
   if (rc != FSEM_OK) return rc;
-  rc = stoi::run_tail(batch, g, rows, w.y10, w.vad, w.idx, w.kept, w.tob, g.tmax, nullptr, nullptr, st);
+  rc = stoi::run_tail(batch, g, rows, w.y10, w.vad, w.idx, w.kept, w.tob, g.tmax, w.part, nullptr, nullptr, st);
   if (rc != FSEM_OK) return rc;
   rc = stream_wait(side, st);
   if (rc != FSEM_OK) return rc;
   rc = pesq::run_wb_back(batch, length, lengths, mos, ws, side);
   if (rc != FSEM_OK) return rc;
-  rc = stoi::run_seg(batch, w.tob, g.tmax, w.kept, stoi_out, estoi_out, st);
+  rc = stoi::run_seg(batch, w.tob, g.tmax, w.kept, w.part, stoi_out, estoi_out, st);
   const int rj = stream_wait(st, side);
   return rc != FSEM_OK ? rc : rj;
 }

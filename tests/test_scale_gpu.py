@@ -4,8 +4,10 @@ entry the bench times, checked by size-independent properties:
 
 * rows spread over the batch (first, middle, last) agree with the oracle -- the CPU restatement of
   the reference pinned by tests/golden -- within the parity tolerances;
-* the same rows scored inside a batch of 6 are bitwise those of the 4096-row batch (no state shared
-  across rows, no 32-bit offset wrap);
+* the same rows scored inside a batch of 6 are those of the 4096-row batch (no state shared across
+  rows, no 32-bit offset wrap): STOI / ESTOI bitwise; PESQ within 1e-5, because the PESQ back end
+  spreads an utterance over 4 waves in batches of up to 2 rows per CU and over one wave in larger ones,
+  which changes the summation order of its band totals (pesq.hip, pesq_back);
 * two runs are bitwise identical (deterministic: fixed-order reductions, no atomics);
 * every score is finite and inside the metric's range.
 """
@@ -44,7 +46,8 @@ def test_bench_config_rows_vs_oracle_and_batch_independence(batch):
 
     idx = torch.tensor(ROWS, device="cuda")
     small = [t.cpu().numpy() for t in m.scores(c[idx].contiguous(), n[idx].contiguous())]
-    np.testing.assert_array_equal(small[0], mos[ROWS])
+    np.testing.assert_allclose(small[0], mos[ROWS], rtol=0, atol=1e-5)
+    print(f"4-wave vs 1-wave back end: max |dPESQ| {np.abs(small[0] - mos[ROWS]).max():.2e}")
     np.testing.assert_array_equal(small[1], s[ROWS])
     np.testing.assert_array_equal(small[2], e[ROWS])
 
