@@ -35,6 +35,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 
 #include "fsem_fft.h"
@@ -851,8 +852,9 @@ __device__ __forceinline__ float loud(float p, int b) {
 // summation order of the band totals and of the window L2 sum (~1e-7 relative in the score).
 template <int BW>
 __global__ void __launch_bounds__(64 * BW) __attribute__((amdgpu_waves_per_eu(4)))
-    pesq_back(const float *__restrict__ bark, const float *__restrict__ power, int64_t B, int64_t Lcap,
-              const int32_t *__restrict__ lens, int Fcap, float *__restrict__ scratch, float *__restrict__ mos) {
+    pesq_back(const float *__restrict__ bark, const float *__restrict__ power, const float *__restrict__ ppart,
+              int nseg, int64_t B, int64_t Lcap, const int32_t *__restrict__ lens, int Fcap,
+              float *__restrict__ scratch, float *__restrict__ mos) {
   constexpr int BT = 64 * BW;
   const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t b = blockIdx.x;
@@ -885,8 +887,26 @@ __global__ void __launch_bounds__(64 * BW) __attribute__((amdgpu_waves_per_eu(4)
   float *__restrict__ asym = sym + F;
   int *__restrict__ keepf = reinterpret_cast<int *>(sym + 2 * (int64_t)Fcap);
   // PESQ.py:97-100 -- power = sum / (L + 5120) / 1.04684; bark scales by 1e7 / power
-  const float pc = power[b] / (float)(L + 5120) / 1.04684f;
-  const float pn = power[b + B] / (float)(L + 5120) / 1.04684f;
+  // signal powers: given, or (ppart != nullptr, the whole-metric entries) summed here from the
+  // front end's per-segment partials in pesq_power_sum's order -- one launch fewer per call
+  float pwc, pwn;
+  if (ppart) {
+    __shared__ float pw_s[2];
+    if (tid < 2) {
+      const float *__restrict__ q = ppart + (b + tid * B) * (int64_t)nseg * 4;
+      float acc = 0.f;
+      for (int g = 0; g < 4 * nseg; ++g) acc += q[g];
+      pw_s[tid] = acc;
+    }
+    lds_barrier();
+    pwc = pw_s[0];
+    pwn = pw_s[1];
+  } else {
+    pwc = power[b];
+    pwn = power[b + B];
+  }
+  const float pc = pwc / (float)(L + 5120) / 1.04684f;
+  const float pn = pwn / (float)(L + 5120) / 1.04684f;
   const float sc = 1e7f / pc, sn = 1e7f / pn;
   const int nch = (F + 63) / 64;
 
@@ -1104,15 +1124,15 @@ extern "C" size_t fsem_pesq_workspace_bytes(int64_t batch, int64_t length) {
 
 int fsem::pesq::launch_front(const float *ref, const float *deg, int64_t batch, int64_t length, int64_t ld,
                              const int32_t *lengths, float *bark, float *power, void *ws, size_t ws_bytes,
-                             float *y10, int64_t y_ld, float2 *vad, int64_t v_ld, hipStream_t st) {
-  if (!ref || !deg || !bark || !power || batch <= 0 || length <= 0 || ld < length || length > kMaxLength)
+                             float *y10, int64_t y_ld, float2 *vad, int64_t v_ld, hipStream_t st,
+                             bool power_sums) {
+  if (!ref || !deg || !bark || (power_sums && !power) || batch <= 0 || length <= 0 || ld < length || length > kMaxLength)
     return FSEM_EINVAL;
   const pesq::Geometry g = pesq::geometry(length);
   if (g.F < 20 && !lengths) return FSEM_ESHORT;
   if (ws_bytes < fsem_pesq_front_workspace_bytes(batch, length) || !ws) return FSEM_EWORKSPACE;
   const int64_t nitems = 2 * batch * (int64_t)g.nseg;
-  int dev = 0, ncu = 256;
-  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  const int ncu = cu_count();
   // 2 resident workgroups per CU; FSEM_FRONT_WGS_PER_CU (diagnostics only) overrides
   static const int wgs_per_cu = [] {
     const char *e = getenv("FSEM_FRONT_WGS_PER_CU");
@@ -1133,6 +1153,7 @@ int fsem::pesq::launch_front(const float *ref, const float *deg, int64_t batch, 
   }
 #undef FSEM_FRONT
   FSEM_CHECK_LAUNCH();
+  if (!power_sums) return FSEM_OK;  // the back end sums the partials itself
   hipLaunchKernelGGL(pesq::pesq_power_sum, dim3((unsigned)((2 * batch + 255) / 256)), dim3(256), 0, st,
                      ppart, g.nseg, 2 * batch, power);
   FSEM_CHECK_LAUNCH();
@@ -1156,39 +1177,61 @@ extern "C" int fsem_pesq_front_y10_f32(const float *ref, const float *deg, int64
                             reinterpret_cast<float2 *>(vad), vad_ld, (hipStream_t)stream);
 }
 
+size_t fsem::pesq::back_keep_bytes(int64_t length) {
+  return sizeof(unsigned long long) * (size_t)((pesq::geometry(length).F + 63) / 64);
+}
+
+// Waves per utterance of the back end: several for small batches, where one utterance's latency
+// is the call's (10 s rows, B = 256: 4 waves 0.083 ms vs one 0.100 ms; 16 s rows, B = 64: PESQ
+// call 0.268 ms with 4 waves, 0.232 ms with 8, which a joint call at B = 256 loses back by
+// crowding the STOI kernels beside it: 8 up to half a row per CU, then 4); one wave once the batch
+// gives every CU more than 2 rows (from B = 1024 one wave is as fast or faster, and leaves more
+// room to the STOI segment kernel beside it in the joint entry); one wave also needs its keep
+// ballots in LDS.  FSEM_BACK_WAVES (diagnostics only) forces 1, 4 or 8.
+int fsem::pesq::back_waves(int64_t batch, int64_t length) {
+  static const int forced = [] {
+    const char *e = getenv("FSEM_BACK_WAVES");
+    const int v = e ? atoi(e) : 0;
+    return (v == 1 || v == 4 || v == 8) ? v : 0;
+  }();
+  const bool fits = back_keep_bytes(length) <= 32768;
+  if (forced) return (forced == 1 && !fits) ? 4 : forced;
+  const int ncu = cu_count();
+  if (fits && batch > 2 * (int64_t)ncu) return 1;
+  return batch > ncu / 2 ? 4 : 8;
+}
+
 extern "C" size_t fsem_pesq_back_workspace_bytes(int64_t batch, int64_t length) {
   const pesq::Geometry g = pesq::geometry(length);
   return align_up(sizeof(float) * (size_t)batch * (size_t)g.F * 4, 256);
 }
 
-extern "C" int fsem_pesq_back_f32(const float *bark, const float *power, int64_t batch, int64_t length,
-                                  const int32_t *lengths, float *mos, void *ws, size_t ws_bytes,
-                                  void *stream) {
-  if (!bark || !power || !mos || batch <= 0 || length <= 0 || length > kMaxLength) return FSEM_EINVAL;
+int fsem::pesq::launch_back(const float *bark, const float *power, const float *ppart, int64_t batch,
+                            int64_t length, const int32_t *lengths, float *mos, void *ws, size_t ws_bytes,
+                            hipStream_t stream) {
+  if (!bark || (!power && !ppart) || !mos || batch <= 0 || length <= 0 || length > kMaxLength) return FSEM_EINVAL;
   const pesq::Geometry g = pesq::geometry(length);
   if (g.F < 20 && !lengths) return FSEM_ESHORT;
   if (!ws || ws_bytes < fsem_pesq_back_workspace_bytes(batch, length)) return FSEM_EWORKSPACE;
   if (batch > 0x7fffffff) return FSEM_EINVAL;
-  // 4 waves per utterance for batches up to 2 rows per CU (measured: 10 s rows, B = 256 --
-  // 0.083 vs 0.100 ms; from B = 1024 on the one-wave form is as fast or faster, and leaves more
-  // room to the STOI segment kernel beside it in the joint entry); one wave also needs its keep
-  // ballots in LDS.  FSEM_BACK_WAVES (diagnostics only) forces 1 or 4.
-  int dev = 0, ncu = 256;
-  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-  static const int forced = [] {
-    const char *e = getenv("FSEM_BACK_WAVES");
-    return e ? atoi(e) : 0;
-  }();
-  const size_t keep_bytes = sizeof(unsigned long long) * (size_t)((g.F + 63) / 64);
-  const bool wide = keep_bytes > 32768 || (forced ? forced == 4 : batch <= 2 * (int64_t)ncu);
-  if (wide)
-    hipLaunchKernelGGL(pesq::pesq_back<4>, dim3((unsigned)batch), dim3(256), 0, (hipStream_t)stream, bark, power,
-                       batch, length, lengths, g.F, static_cast<float *>(ws), mos);
-  else
-    hipLaunchKernelGGL(pesq::pesq_back<1>, dim3((unsigned)batch), dim3(64), keep_bytes, (hipStream_t)stream, bark, power,
-                       batch, length, lengths, g.F, static_cast<float *>(ws), mos);
+  const int bw = pesq::back_waves(batch, length);
+  float *scratch = static_cast<float *>(ws);
+#define FSEM_BACK(W, LDS)                                                                                    \
+  hipLaunchKernelGGL(pesq::pesq_back<W>, dim3((unsigned)batch), dim3(64 * W), LDS, stream, bark, power, ppart, \
+                     g.nseg, batch, length, lengths, g.F, scratch, mos)
+  if (bw == 8) FSEM_BACK(8, 0);
+  else if (bw == 4) FSEM_BACK(4, 0);
+  else FSEM_BACK(1, pesq::back_keep_bytes(length));
+#undef FSEM_BACK
   FSEM_CHECK_LAUNCH();
   return FSEM_OK;
+}
+
+extern "C" int fsem_pesq_back_f32(const float *bark, const float *power, int64_t batch, int64_t length,
+                                  const int32_t *lengths, float *mos, void *ws, size_t ws_bytes,
+                                  void *stream) {
+  if (!power) return FSEM_EINVAL;
+  return pesq::launch_back(bark, power, nullptr, batch, length, lengths, mos, ws, ws_bytes, (hipStream_t)stream);
 }
 
 hipStream_t fsem::side_stream(hipStream_t st) {
@@ -1210,11 +1253,38 @@ hipStream_t fsem::side_stream(hipStream_t st) {
 
 int fsem::stream_wait(hipStream_t waiter, hipStream_t producer) {
   if (waiter == producer) return FSEM_OK;
-  hipEvent_t ev;  // one event per edge: concurrent callers never share a record
-  if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return FSEM_ELAUNCH;
-  const bool ok = hipEventRecord(ev, producer) == hipSuccess && hipStreamWaitEvent(waiter, ev, 0) == hipSuccess;
-  (void)hipEventDestroy(ev);  // released once the recorded work completes
+  // one event per (host thread, device), recorded anew for every edge: a wait enqueued earlier
+  // keeps the record it was enqueued behind, and no other thread records this event
+  constexpr int kMaxDev = 64;
+  thread_local hipEvent_t ev[kMaxDev] = {};
+  hipDevice_t dev = 0;
+  if (hipStreamGetDevice(producer, &dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return FSEM_ELAUNCH;
+  if (!ev[dev]) {
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess) return FSEM_ELAUNCH;
+    if (cur != dev && hipSetDevice(dev) != hipSuccess) return FSEM_ELAUNCH;
+    const bool made = hipEventCreateWithFlags(&ev[dev], hipEventDisableTiming) == hipSuccess;
+    if (cur != dev) (void)hipSetDevice(cur);
+    if (!made) {
+      ev[dev] = nullptr;
+      return FSEM_ELAUNCH;
+    }
+  }
+  const bool ok = hipEventRecord(ev[dev], producer) == hipSuccess && hipStreamWaitEvent(waiter, ev[dev], 0) == hipSuccess;
   return ok ? FSEM_OK : FSEM_ELAUNCH;
+}
+
+int fsem::cu_count() {
+  constexpr int kMaxDev = 64;
+  static std::atomic<int> cache[kMaxDev];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return 256;
+  int n = cache[dev].load(std::memory_order_relaxed);
+  if (n > 0) return n;
+  n = 256;
+  (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+  cache[dev].store(n, std::memory_order_relaxed);
+  return n;
 }
 
 // Workspace of the whole-metric entry: [front partials | bark | power | back scratch].
@@ -1245,15 +1315,16 @@ int fsem::pesq::run_wb_front(const float *ref, const float *deg, int64_t batch, 
   if (!ws || ws_bytes < fsem_pesq_workspace_bytes(batch, length)) return FSEM_EWORKSPACE;
   const WbWs w = carve_wb(ws, batch, length);
   return pesq::launch_front(ref, deg, batch, length, ld, lengths, w.bark, w.power, ws, w.front, y10, y_ld, vad,
-                            v_ld, stream);
+                            v_ld, stream, /*power_sums=*/false);
 }
 
 int fsem::pesq::run_wb_back(int64_t batch, int64_t length, const int32_t *lengths, float *mos, void *ws,
                             hipStream_t back_st) {
   if (!mos) return FSEM_EINVAL;
   const WbWs w = carve_wb(ws, batch, length);
-  return fsem_pesq_back_f32(w.bark, w.power, batch, length, lengths, mos, w.back,
-                            fsem_pesq_back_workspace_bytes(batch, length), back_st);
+  // the front end's per-segment power partials sit at the start of the workspace (launch_front)
+  return pesq::launch_back(w.bark, nullptr, static_cast<const float *>(ws), batch, length, lengths, mos, w.back,
+                           fsem_pesq_back_workspace_bytes(batch, length), back_st);
 }
 
 int fsem::pesq::run_wb(const float *ref, const float *deg, int64_t batch, int64_t length, int64_t ld,

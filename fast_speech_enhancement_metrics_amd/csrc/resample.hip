@@ -9,11 +9,13 @@
 // _get_sinc_resample_kernel (including its float32 phase offsets) and passed by value.
 #include <math.h>
 
+#include <mutex>
+
 #include "fsem_resample.h"
 
 namespace fsem {
 
-int make_resample_kernel(int32_t orig_freq, int32_t new_freq, ResampleKernel *rk) {
+static int build_resample_kernel(int32_t orig_freq, int32_t new_freq, ResampleKernel *rk) {
   if (orig_freq <= 0 || new_freq <= 0) return FSEM_ERATE;
   int32_t a = orig_freq, b = new_freq;
   while (b) {
@@ -35,6 +37,34 @@ int make_resample_kernel(int32_t orig_freq, int32_t new_freq, ResampleKernel *rk
   if (rk->big) return FSEM_OK;  // coefficients built on the device (resample_sinc_lds)
   for (int j = 0; j < nw; ++j)
     for (int t = 0; t < taps; ++t) rk->k[j * taps + t] = sinc_coef(j, t, orig, nw, width);
+  return FSEM_OK;
+}
+
+// The kernels of the last few rate pairs, kept so a call does not re-evaluate ~nw * taps float64
+// sinc / cos terms (16 -> 10 kHz: 140) on the host each time.
+int make_resample_kernel(int32_t orig_freq, int32_t new_freq, ResampleKernel *rk) {
+  constexpr int kSlots = 8;
+  struct Slot {
+    int32_t orig_freq, new_freq;
+    ResampleKernel rk;
+  };
+  static std::mutex mu;
+  static Slot slots[kSlots];
+  static int used = 0, next = 0;
+  {
+    std::lock_guard<std::mutex> lock(mu);
+    for (int i = 0; i < used; ++i)
+      if (slots[i].orig_freq == orig_freq && slots[i].new_freq == new_freq) {
+        *rk = slots[i].rk;
+        return FSEM_OK;
+      }
+  }
+  const int rc = build_resample_kernel(orig_freq, new_freq, rk);
+  if (rc != FSEM_OK) return rc;
+  std::lock_guard<std::mutex> lock(mu);
+  slots[next] = Slot{orig_freq, new_freq, *rk};
+  next = (next + 1) % kSlots;
+  if (used < kSlots) ++used;
   return FSEM_OK;
 }
 

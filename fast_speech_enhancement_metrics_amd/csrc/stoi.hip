@@ -708,8 +708,7 @@ inline int run(const float *ref, const float *deg, int64_t B, int64_t length, in
   if (g.mode == 0) {
     const int nchunk = (int)((g.L10 + VF2 * 128 - 1) / (VF2 * 128));
     const int64_t nitems = B * (int64_t)nchunk * 2;
-    int dev = 0, ncu = 256;
-    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const int ncu = cu_count();
     const int64_t grid = nitems < (int64_t)ncu * 3 ? nitems : (int64_t)ncu * 3;  // 3 resident per CU
     hipLaunchKernelGGL(stoi_resample_vad16, dim3((unsigned)grid), dim3(256), 0, st, ref, deg, rows, ld, nchunk,
                        nitems, w.y10, g.y_ld, w.vad, g.v_ld);
@@ -791,20 +790,32 @@ extern "C" int fsem_pesq_stoi_f32(const float *ref, const float *deg, int64_t ba
   stoi::Ws w = stoi::carve(static_cast<char *>(ws) + pesq_bytes, batch, g);
   const stoi::Rows rows{lengths, length, rk.orig, rk.nw};
   hipStream_t st = (hipStream_t)stream;
-  // PESQ-wb with the 10 kHz rows emitted from the same input tiles.  The PESQ back end (one
-  // wave per pair) runs on a side stream concurrently with the STOI segment kernel (VALU bound,
-  // where the back end's latency-bound waves fit in better than beside the LDS-bound stoi_tob);
-  // both only read what the front end wrote, and the caller's stream joins the side stream.
+  // PESQ-wb with the 10 kHz rows emitted from the same input tiles; the PESQ back end runs on a
+  // side stream concurrently with the STOI tail, and the caller's stream joins the side stream.
+  // Large batches start the back end (one wave per pair) beside the STOI segment kernel (VALU
+  // bound, where its latency-bound waves fit in better than beside the LDS-bound stoi_tob); small
+  // batches (several waves per pair) start it as soon as the front end is done, beside
+  // stoi_select / stoi_tob, since neither fills the chip.  Both only read what the front end wrote.
   const hipStream_t side = side_stream(st);
+  const bool early = pesq::back_waves(batch, length) > 1;
   rc = pesq::run_wb_front(ref, deg, batch, length, ld, lengths, ws, pesq_bytes, w.y10, g.y_ld, w.vad, g.v_ld, st);
   if (rc != FSEM_OK) return rc;
-  rc = stoi::run_tail(batch, g, rows, w.y10, w.vad, w.idx, w.kept, w.tob, g.tmax, w.part, nullptr, nullptr, st);
-  if (rc != FSEM_OK) return rc;
-  rc = stream_wait(side, st);
-  if (rc != FSEM_OK) return rc;
-  rc = pesq::run_wb_back(batch, length, lengths, mos, ws, side);
-  if (rc != FSEM_OK) return rc;
-  rc = stoi::run_seg(batch, w.tob, g.tmax, w.kept, w.part, stoi_out, estoi_out, st);
+  if (early) {
+    rc = stream_wait(side, st);
+    if (rc != FSEM_OK) return rc;
+    rc = pesq::run_wb_back(batch, length, lengths, mos, ws, side);
+    if (rc != FSEM_OK) return rc;
+    rc = stoi::run_tail(batch, g, rows, w.y10, w.vad, w.idx, w.kept, w.tob, g.tmax, w.part, stoi_out, estoi_out,
+                        st);
+  } else {
+    rc = stoi::run_tail(batch, g, rows, w.y10, w.vad, w.idx, w.kept, w.tob, g.tmax, w.part, nullptr, nullptr, st);
+    if (rc != FSEM_OK) return rc;
+    rc = stream_wait(side, st);
+    if (rc != FSEM_OK) return rc;
+    rc = pesq::run_wb_back(batch, length, lengths, mos, ws, side);
+    if (rc != FSEM_OK) return rc;
+    rc = stoi::run_seg(batch, w.tob, g.tmax, w.kept, w.part, stoi_out, estoi_out, st);
+  }
   const int rj = stream_wait(st, side);
   return rc != FSEM_OK ? rc : rj;
 }
