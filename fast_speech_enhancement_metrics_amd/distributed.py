@@ -126,3 +126,65 @@ def sharded_scores_ragged(metric, clean, noisy, group=None, device=None) -> torc
         if idx:
             full[torch.tensor(idx, device=coll)] = out[r * cap:r * cap + len(idx)]
     return full
+
+
+def scatter_batch(clean, noisy, src: int = 0, group=None, lengths=None, device=None):
+    """Inputs on one device: rank ``src`` holds the whole [B, L] batch (other ranks
+    pass None); every rank receives its contiguous shard (``shard_bounds``) by point-to-point
+    sends from ``src`` -- over xGMI with RCCL, one link per destination GPU, all in flight at
+    once -- into ``device`` (default: the collective's device).  Returns (clean_shard,
+    noisy_shard, lengths_shard or None, B).  The copy is the only data movement: ``src`` sends
+    views of its rows, no padded staging copy."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    gsrc = dist.get_global_rank(group, src) if group is not None else src
+    dev = collective_device(group, device if device is not None else (noisy.device if noisy is not None else None))
+    # shape, dtype code and whether lengths come along: one small broadcast
+    dtypes = [torch.float32, torch.float16, torch.bfloat16, torch.float64]
+    meta = torch.zeros(4, dtype=torch.int64, device=dev)
+    if rank == src:
+        if clean.shape != noisy.shape or clean.dim() != 2:
+            raise ValueError("scatter_batch: clean / noisy must be [B, L] of one shape")
+        meta[0], meta[1] = clean.shape[0], clean.shape[1]
+        meta[2] = dtypes.index(noisy.dtype)
+        meta[3] = 0 if lengths is None else 1
+    dist.broadcast(meta, gsrc, group=group)
+    B, L, code, has_len = (int(v) for v in meta.tolist())
+    dtype = dtypes[code]
+    lens_all = torch.empty(B, dtype=torch.int64, device=dev)
+    if has_len:
+        if rank == src:
+            lens_all.copy_(torch.as_tensor(lengths).reshape(-1).to(torch.int64))
+        dist.broadcast(lens_all, gsrc, group=group)
+    lo, hi = shard_bounds(B, world, rank)
+    ops = []
+    if rank == src:
+        c_src, n_src = clean.to(dev), noisy.to(dev)
+        for r in range(world):
+            if r == src:
+                continue
+            a, b = shard_bounds(B, world, r)
+            if b > a:
+                peer = dist.get_global_rank(group, r) if group is not None else r
+                ops.append(dist.P2POp(dist.isend, c_src[a:b].contiguous(), peer, group=group))
+                ops.append(dist.P2POp(dist.isend, n_src[a:b].contiguous(), peer, group=group))
+        c_loc, n_loc = c_src[lo:hi], n_src[lo:hi]
+    else:
+        c_loc = torch.empty(hi - lo, L, dtype=dtype, device=dev)
+        n_loc = torch.empty(hi - lo, L, dtype=dtype, device=dev)
+        if hi > lo:
+            ops.append(dist.P2POp(dist.irecv, c_loc, gsrc, group=group))
+            ops.append(dist.P2POp(dist.irecv, n_loc, gsrc, group=group))
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+    lens_loc = lens_all[lo:hi] if has_len else None
+    return c_loc, n_loc, lens_loc, B
+
+
+def sharded_scores_from(metric, clean, noisy, src: int = 0, group=None, lengths=None, device=None) -> torch.Tensor:
+    """``sharded_scores`` for a batch that lives on rank ``src`` only: scatter the shards
+    (``scatter_batch``), score them, all-gather the scores -> [B, k] on every rank."""
+    c, n, lens, B = scatter_batch(clean, noisy, src=src, group=group, lengths=lengths, device=device)
+    local = _local_scores(metric, c, n, lens, collective_device(group, c.device))
+    return gather_scores(local, B, group)

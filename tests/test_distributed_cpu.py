@@ -204,3 +204,55 @@ def test_empty_shards():
         np.testing.assert_allclose(p[:, 0], ref_p, atol=1e-6, rtol=0)
         np.testing.assert_allclose(pr[:, 0], ref_p, atol=1e-6, rtol=0)
         np.testing.assert_allclose(s, ref_s, atol=1e-6, rtol=0)
+
+
+def _scatter_worker(rank, world, port, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from fast_speech_enhancement_metrics_amd import PESQ_STOI
+        from fast_speech_enhancement_metrics_amd.distributed import scatter_batch, sharded_scores_from
+        from fast_speech_enhancement_metrics_amd.synthetic import speech_like_pairs
+        src = 1
+        c = n = lens = None
+        if rank == src:  # only the source rank holds the batch
+            c, n, _ = speech_like_pairs(5, 24000, 16000, seed=3)
+            lens = torch.tensor([24000, 20000, 24000, 9000, 16001], dtype=torch.int32)
+        cs, ns, ls, B = scatter_batch(c, n, src=src, lengths=lens)
+        s = sharded_scores_from(PESQ_STOI(16000), c, n, src=src, lengths=lens)
+        out_q.put((rank, B, cs.numpy(), ns.numpy(), ls.numpy(), s.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_scatter_from_one_rank(world):
+    """Inputs held by one rank: each rank receives exactly its shard_bounds rows and
+    lengths, and the scattered, sharded, gathered scores equal the single-process result."""
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_scatter_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    from fast_speech_enhancement_metrics_amd import PESQ_STOI
+    from fast_speech_enhancement_metrics_amd.distributed import shard_bounds
+    from fast_speech_enhancement_metrics_amd.synthetic import speech_like_pairs
+    c, n, _ = speech_like_pairs(5, 24000, 16000, seed=3)
+    lens = torch.tensor([24000, 20000, 24000, 9000, 16001], dtype=torch.int32)
+    ref = torch.stack(PESQ_STOI(16000).scores(c, n, lengths=lens), 1).numpy()
+    for rank, B, cs, ns, ls, s in res:
+        lo, hi = shard_bounds(5, world, rank)
+        assert B == 5
+        np.testing.assert_array_equal(cs, c[lo:hi].numpy())
+        np.testing.assert_array_equal(ns, n[lo:hi].numpy())
+        np.testing.assert_array_equal(ls, lens[lo:hi].numpy())
+        np.testing.assert_allclose(s, ref, rtol=0, atol=1e-6, equal_nan=True)
