@@ -311,6 +311,11 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     distributed = "WORLD_SIZE" in os.environ  # launched by torch.distributed.run (any N)
     if distributed:
+        # RCCL prints a version banner on the process's stdout at init: route native stdout to
+        # stderr so the result line stays the only line on stdout
+        out_fd = os.dup(1)
+        os.dup2(2, 1)
+        sys.stdout = os.fdopen(out_fd, "w", buffering=1)
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
