@@ -292,6 +292,35 @@ __device__ unsigned long long g_tob_stamps[kTobStampBlocks][4];
   } while (0)
 #endif
 
+// Peak biased float exponents of a wave's clean and denoised samples (0: all zero or
+// denormal), packed (clean << 16 | denoised): per-lane maxima, then a DPP reduction (row
+// rotations, row broadcasts) with a packed 16-bit max -- both signals per instruction, no LDS --
+// whose last lane holds the wave's maxima (uniform result).
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t peak_exponents(float c0, float c1, float c2, float c3, float d0, float d1,
+                                                   float d2, float d3) {
+  typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+  // exponent field of the larger magnitude (integer max of |x|'s bits: same order as magnitude)
+  auto mx = [](float a, float b) { return max(__float_as_uint(a) & 0x7fffffffu, __float_as_uint(b) & 0x7fffffffu); };
+  const uint32_t mc = max(mx(c0, c1), mx(c2, c3)), md = max(mx(d0, d1), mx(d2, d3));
+  uint32_t e = ((mc >> 7) & 0xffff0000u) | (md >> 23);
+  auto pmax = [](uint32_t x, uint32_t y) {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(us2, x), __builtin_bit_cast(us2, y)));
+  };
+  e = pmax(e, dpp_u<0x121>(e));  // row_ror:1
+  e = pmax(e, dpp_u<0x122>(e));  // row_ror:2
+  e = pmax(e, dpp_u<0x124>(e));  // row_ror:4
+  e = pmax(e, dpp_u<0x128>(e));  // row_ror:8 -> every lane holds its row's maxima
+  // rows 1 and 3 take rows 0 and 2 (row_bcast:15), rows 2 and 3 take lane 31 (row_bcast:31);
+  // rows outside the mask read 0, the identity of the max
+  e = pmax(e, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)e, 0x142, 0xA, 0xF, false));
+  e = pmax(e, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)e, 0x143, 0xC, 0xF, false));
+  return __builtin_amdgcn_readlane(e, 63);
+}
+
 constexpr int TOB_WAVES = 4;  // 256-thread workgroups (8 waves x 66 KB measured no faster)
 __global__ void __launch_bounds__(64 * TOB_WAVES)
     stoi_tob(const float *__restrict__ y10, int64_t y_ld, int64_t B, Rows rows, const int *__restrict__ idx,
@@ -386,10 +415,26 @@ __global__ void __launch_bounds__(64 * TOB_WAVES)
     // rounding is not exactly Hermitian: ~1e-7 of the other signal's spectrum would leak into
     // it, and the segment normalisation (STOI.py:113-119) would turn that leak into a
     // correlation (an all-zero denoised signal would score ~0.8 instead of 0).
-    const bool c_zero = !__any(v[0].r != 0.f || v[1].r != 0.f || v[2].r != 0.f || v[3].r != 0.f);
-    const bool d_zero = !__any(v[0].i != 0.f || v[1].i != 0.f || v[2].i != 0.f || v[3].i != 0.f);
-    // wave-uniform factors (SGPR operands of the final multiply): 0.25, or 0 for a zero frame
-    const float c_scale = c_zero ? 0.f : 0.25f, d_scale = d_zero ? 0.f : 0.25f;
+    // The same rounding leaks ~1e-7 of the louder signal's spectrum into the quieter one's
+    // whatever their levels, so a frame whose denoised signal sits ~100 dB or more below the clean
+    // one (e.g. int16-scaled clean against float denoised) would lose its spectrum to the leak.
+    // Frames with a gap of 2^7 or more in peak sample are equalised first: the denoised half is
+    // scaled by 2^sh to the clean half's peak exponent (exact in floating point), its power by
+    // 2^-2sh after the FFT (exact again).
+    const uint32_t pk = peak_exponents(v[0].r, v[1].r, v[2].r, v[3].r, v[0].i, v[1].i, v[2].i, v[3].i);
+    const int ec = (int)(pk >> 16), ed = (int)(pk & 0xffffu);
+    const bool c_zero = ec == 0 && !__any(v[0].r != 0.f || v[1].r != 0.f || v[2].r != 0.f || v[3].r != 0.f);
+    const bool d_zero = ed == 0 && !__any(v[0].i != 0.f || v[1].i != 0.f || v[2].i != 0.f || v[3].i != 0.f);
+    int sh = (ec > 0 && ed > 0) ? ec - ed : 0;
+    sh = (sh >= 7 || sh <= -7) ? max(-60, min(60, sh)) : 0;
+    if (sh != 0) {  // uniform
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r].i = __builtin_amdgcn_ldexpf(v[r].i, sh);
+    }
+    // wave-uniform factors (SGPR operands of the final multiply): 0.25 (x 2^-2k for the denoised
+    // power), or 0 for a zero frame
+    const float c_scale = c_zero ? 0.f : 0.25f;
+    const float d_scale = d_zero ? 0.f : __builtin_amdgcn_ldexpf(0.25f, -2 * sh);
     fft512_wave(v, wbuf, lane, tw1, tw2);
     float pc[4], pd[4];
 #pragma unroll
