@@ -257,9 +257,16 @@ __global__ void __launch_bounds__(256)
   const int NV = rows.nv(b);
   const float2 *__restrict__ q = vad + b * v_ld;
   float m = -INFINITY;
-  for (int i = tid; i < NV; i += 256) m = fmaxf(m, vad_energy_db(q, i));
+  int nan_seen = 0;
+  for (int i = tid; i < NV; i += 256) {
+    const float e = vad_energy_db(q, i);
+    m = fmaxf(m, e);
+    nan_seen |= (e != e);
+  }
   m = block_max_256(m, red);
-  const float thr = m - 40.f;  // (max - dynamic_range - e) < 0  (STOI.py:102)
+  // a NaN energy (a NaN clean sample) makes torch's max NaN, so no frame passes the test and the
+  // row has no segments (STOI NaN); fmaxf alone would skip it
+  const float thr = __syncthreads_or(nan_seen) ? __builtin_nanf("") : m - 40.f;  // (max - dynamic_range - e) < 0  (STOI.py:102)
   int base = 0;
   for (int i0 = 0; i0 < NV; i0 += 256) {
     const int i = i0 + tid;
