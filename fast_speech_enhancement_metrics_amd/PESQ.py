@@ -20,6 +20,34 @@ class PESQ(BaseMetric):
     def __init__(self, sample_rate: int = 16000, use_gpu: bool = False):
         super().__init__(sample_rate, use_gpu)
 
+    # ------------------------------------------------------------------ reference attributes
+    # The reference's filter coefficients (PESQ.py:79-90), float32 on the metric's device, built
+    # on first access (the engine carries its own copies in constant memory).
+    @property
+    def power_filter(self) -> torch.Tensor:
+        """[2, 11] (b; a) of the order-5 Butterworth band-pass 325-3250 Hz at 16 kHz (PESQ.py:80-81)."""
+        if getattr(self, "_power_filter", None) is None:
+            import numpy as np
+            from scipy.signal import butter
+            out = np.asarray(butter(5, [325, 3250], fs=16000, btype="band"))
+            self._power_filter = torch.as_tensor(out, device=self.device, dtype=torch.float32)
+        return self._power_filter
+
+    @property
+    def pre_filter(self) -> torch.Tensor:
+        """[2, 3] (b; a) of the pre-emphasis IIR (PESQ.py:84-88)."""
+        if getattr(self, "_pre_filter", None) is None:
+            self._pre_filter = torch.tensor([[2.740826, -5.4816519, 2.740826], [1.0, -1.9444777, 0.94597794]],
+                                            device=self.device, dtype=torch.float32)
+        return self._pre_filter
+
+    @property
+    def taper_weights(self) -> torch.Tensor:
+        """[15] edge taper (k + 1) / 16 of the first / last 15 samples (PESQ.py:90)."""
+        if getattr(self, "_taper_weights", None) is None:
+            self._taper_weights = torch.linspace(0, 15, 16, device=self.device)[1:] / 16.0
+        return self._taper_weights
+
     # ------------------------------------------------------------------ device paths
     def scores(self, clean_speech: torch.Tensor, denoised_speech: torch.Tensor, lengths=None,
                sample_rate: int | None = None) -> torch.Tensor:

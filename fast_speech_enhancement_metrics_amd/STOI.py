@@ -32,6 +32,27 @@ class STOI(BaseMetric):
         self.beta = -15.0
         self.dynamic_range = 40
 
+    # ------------------------------------------------------------------ reference attributes
+    def get_octave_band_matrix(self) -> torch.Tensor:
+        """[15, 257] float32 1/3-octave band matrix (STOI.py:26-47): band i covers the FFT bins
+        from the one nearest 150 * 2^((2i - 1) / 6) Hz up to (excluding) the one nearest
+        150 * 2^((2i + 1) / 6) Hz."""
+        return _cpu._OBM.to(torch.float32).clone()
+
+    @property
+    def octave_band_matrix(self) -> torch.Tensor:
+        """STOI.py:19, on the metric's device (built on first access)."""
+        if getattr(self, "_octave_band_matrix", None) is None:
+            self._octave_band_matrix = self.get_octave_band_matrix().to(self.device)
+        return self._octave_band_matrix
+
+    @property
+    def window(self) -> torch.Tensor:
+        """[256] float32 analysis window hann(257)[1:] (STOI.py:24), on the metric's device."""
+        if getattr(self, "_window", None) is None:
+            self._window = torch.hann_window(self.win_length + 1, dtype=torch.float32, device=self.device)[1:]
+        return self._window
+
     def scores(self, clean_speech: torch.Tensor, denoised_speech: torch.Tensor, sample_rate: int | None = None,
                lengths=None):
         """(stoi[B], estoi[B]) tensors on the metric's device; NaN where no segment exists.
