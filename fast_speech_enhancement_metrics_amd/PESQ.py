@@ -20,6 +20,13 @@ class PESQ(BaseMetric):
     def __init__(self, sample_rate: int = 16000, use_gpu: bool = False):
         super().__init__(sample_rate, use_gpu)
 
+    @staticmethod
+    def equalize_ranges(clean_speech: torch.Tensor, noisy_speech: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+        """Both rows divided by their joint peak |x| (PESQ.py:115-121).  The engine skips this step:
+        it cancels under the level alignment (amplitude range)."""
+        m = torch.maximum(clean_speech.abs().amax(dim=1, keepdim=True), noisy_speech.abs().amax(dim=1, keepdim=True))
+        return clean_speech / m, noisy_speech / m
+
     # ------------------------------------------------------------------ reference attributes
     # The reference's filter coefficients (PESQ.py:79-90), float32 on the metric's device, built
     # on first access (the engine carries its own copies in constant memory).

@@ -32,6 +32,16 @@ class STOI(BaseMetric):
         self.beta = -15.0
         self.dynamic_range = 40
 
+    @staticmethod
+    def normalize(x: torch.Tensor, dim: int = 0) -> torch.Tensor:
+        """In place, as STOI.py:113-119: centre along ``dim`` and divide by the L2 norm.  Without the
+        reference's ``1e-12 * randn`` term (deterministic, as the engine): a zero-variance slice
+        becomes 0 instead of a random unit vector."""
+        x -= x.mean(dim=dim, keepdim=True)
+        n = torch.linalg.vector_norm(x, ord=2, dim=dim, keepdim=True)
+        x.copy_(torch.where(n > 0, x / torch.where(n > 0, n, torch.ones_like(n)), torch.zeros_like(x)))
+        return x
+
     # ------------------------------------------------------------------ reference attributes
     def get_octave_band_matrix(self) -> torch.Tensor:
         """[15, 257] float32 1/3-octave band matrix (STOI.py:26-47): band i covers the FFT bins

@@ -164,3 +164,20 @@ def test_reference_attributes():
         assert nz[0] == edges[j, 0] and nz[-1] + 1 == edges[j, 1]
     w = s.window
     assert w.shape == (256,) and torch.equal(w, torch.hann_window(257)[1:])
+
+
+def test_reference_static_helpers():
+    """PESQ.equalize_ranges (PESQ.py:115-121) and STOI.normalize (STOI.py:113-119, deterministic)."""
+    from fast_speech_enhancement_metrics_amd import PESQ, STOI
+    g = torch.Generator().manual_seed(0)
+    c, n = torch.randn(3, 100, generator=g), 3 * torch.randn(3, 100, generator=g)
+    c2, n2 = PESQ.equalize_ranges(c, n)
+    peak = torch.maximum(c2.abs().amax(1), n2.abs().amax(1))
+    assert torch.allclose(peak, torch.ones(3))
+    x = torch.randn(4, 30, generator=g)
+    x[1] = 2.0  # zero variance -> 0
+    y = STOI.normalize(x, dim=1)
+    assert y is x
+    assert torch.allclose(x[[0, 2, 3]].mean(1), torch.zeros(3), atol=1e-6)
+    assert torch.allclose(x[[0, 2, 3]].norm(dim=1), torch.ones(3), atol=1e-6)
+    assert (x[1] == 0).all()
