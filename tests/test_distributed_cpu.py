@@ -226,7 +226,7 @@ def _scatter_worker(rank, world, port, out_q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_scatter_from_one_rank(world):
     """Inputs held by one rank: each rank receives exactly its shard_bounds rows and
     lengths, and the scattered, sharded, gathered scores equal the single-process result."""
