@@ -49,8 +49,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=5)
     ap.add_argument("--separate", action="store_true", help="two API calls (PESQ, STOI) instead of the joint entry")
-    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c5"],
-                    help="c2: BASELINE metric (default); c3: STOI+ESTOI only, 8192 x 5 s @ 16 kHz per GPU; "
+    ap.add_argument("--workload", default="c2", choices=["c2", "pesq", "c3", "c5"],
+                    help="c2: BASELINE metric (default, PESQ-wb + STOI/ESTOI); pesq: configs[1] as stated, "
+                         "PESQ-wb only; c3: STOI+ESTOI only, 8192 x 5 s @ 16 kHz per GPU; "
                          "c5: config 5, mixed 8/16 kHz ragged 2-30 s batch")
     return ap.parse_args()
 
@@ -247,6 +248,32 @@ def run_c3(args, world, rank, dev, distributed):
                        "parallelism": f"dp{world}"}}), flush=True)
 
 
+def run_pesq(args, world, rank, dev, distributed):
+    """BASELINE.json configs[1] as stated there: PESQ-wb alone, 4096 x 10 s @ 16 kHz pairs per GPU
+    (PESQ.scores: front end, signal powers folded into the back end, back end).  The headline
+    metric (default workload) adds STOI/ESTOI through the joint entry."""
+    from fast_speech_enhancement_metrics_amd import PESQ
+    from fast_speech_enhancement_metrics_amd.synthetic import speech_like_pairs
+    B, L = 4096, 160000
+    clean, noisy, _ = speech_like_pairs(B, L, 16000, seed=42 + rank, device=dev)
+    pesq = PESQ(16000, use_gpu=True)
+
+    def step():
+        p = pesq.scores(clean, noisy)
+        return p.cpu() if rank == 0 else None
+
+    dt = _timed(step, args, dev, distributed)
+    if rank == 0:
+        print(json.dumps({
+            "metric": "utterances/sec PESQ-wb, 10s@16kHz, batch 4096 (config 2)",
+            "value": round(world * B * args.steps / dt, 2), "unit": "utterances/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic speech-like pairs",
+            "config": {"workload": "config 2: PESQ-wb scores (PESQ.scores)", "batch_per_gpu": B, "length": L,
+                       "sample_rate": 16000, "parallelism": f"dp{world}"}}), flush=True)
+
+
 def run_c5(args, world, rank, dev, distributed):
     """BASELINE.json configs[4] / SURVEY 8(d) C5: 2048 utterances per GPU (16384 on 8), lengths
     uniform in 2-30 s, half at 8 kHz (PESQ via 8->16 kHz, STOI via 8->10 kHz, as the reference's
@@ -321,8 +348,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    if args.workload in ("c3", "c5"):
-        (run_c3 if args.workload == "c3" else run_c5)(args, world, rank, dev, distributed)
+    if args.workload in ("pesq", "c3", "c5"):
+        {"pesq": run_pesq, "c3": run_c3, "c5": run_c5}[args.workload](args, world, rank, dev, distributed)
         if distributed:
             dist.barrier()
             dist.destroy_process_group()

@@ -1,0 +1,46 @@
+"""bench.py's contract pieces that need no GPU: the metric is BASELINE.json's, the defaults are the
+1-GPU headline configuration, the CPU baseline leg returns the contract's fields on a bounded
+sample, and the roofline's traffic comes from the newest committed PMC summary."""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+REPO = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+sys.path.insert(0, REPO)
+import bench  # noqa: E402
+
+
+def test_metric_is_baselines():
+    with open(os.path.join(REPO, "BASELINE.json")) as f:
+        assert bench.METRIC == json.load(f)["metric"]
+
+
+def test_defaults_are_the_headline_config(monkeypatch):
+    monkeypatch.setattr(sys, "argv", ["bench.py"])
+    a = bench.parse()
+    assert (a.gpus, a.batch, a.length, a.workload) == (1, 4096, 160000, "c2")
+    assert a.steps > 0 and a.warmup >= 0 and not a.separate
+
+
+def test_cpu_baseline_fields():
+    from fast_speech_enhancement_metrics_amd.synthetic import speech_like_pairs
+    c, n, _ = speech_like_pairs(2, 16000, 16000, seed=3)
+    out = bench.cpu_baseline(c, n, budget_s=0.0)  # one pair, then the budget stops it
+    assert set(out) == {"value", "unit", "cores", "kind", "sample"}
+    assert out["kind"] == "port" and out["cores"] == 1 and out["unit"] == "utterances/s"
+    assert np.isfinite(out["value"]) and out["value"] > 0
+    assert out["sample"].startswith("1 pairs x 16000 samples")
+    assert torch.get_num_threads() >= 1
+
+
+def test_roofline_traffic_from_newest_pmc_summary():
+    hbm, src = bench.pmc_traffic("pesq_front<true, false>", 4096, 160000)
+    assert hbm is not None and hbm > 5_242_880_000  # at least the algorithmic input bytes
+    rounds = sorted(os.listdir(os.path.join(REPO, "profiles")),
+                    key=lambda p: [int(t) if t.isdigit() else t for t in __import__("re").split(r"(\d+)", p)])
+    newest = [r for r in rounds if os.path.exists(os.path.join(REPO, "profiles", r, "pmc_summary.json"))][-1]
+    assert src == os.path.join("profiles", newest, "pmc_summary.json")
+    assert bench.pmc_traffic("pesq_front<true, false>", 64, 160000) == (None, None)  # other sizes: none
