@@ -467,13 +467,18 @@ __global__ void __launch_bounds__(64 * TOB_WAVES)
       const float *ps = pbuf + 256 * pc_sig;
       float acc = 0.f;
 #pragma unroll
-      for (int i = 0; i < 9; ++i) acc += (pc_lo + i < pc_hi) ? ps[pc_lo + i] : 0.f;
+      for (int i = 0; i < 9; ++i) {  // unconditional reads (inside the signal's 256 powers), masked adds
+        const float x = ps[pc_lo + i];
+        acc += (pc_lo + i < pc_hi) ? x : 0.f;
+      }
 #pragma unroll
       for (int off = 1; off < 8; off <<= 1) {
         const float v = __shfl_down(acc, off, 64);
         if (lane + off < pc_end) acc += v;
       }
-      if (pc_head) tob[((b + pc_sig * B) * NB + pc_band) * tmax + k] = sqrtf(acc);
+      // hardware square root (1 ulp; the correctly rounded sqrtf is a ~17-instruction sequence
+      // that every lane of the wave issues)
+      if (pc_head) tob[((b + pc_sig * B) * NB + pc_band) * tmax + k] = __builtin_amdgcn_sqrtf(acc);
     }
     wave_lds_fence();
   }
