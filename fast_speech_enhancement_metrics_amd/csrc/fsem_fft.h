@@ -82,14 +82,42 @@ __device__ __forceinline__ void dft8v(f2 v[8]) {
   v[7] = FSEM_FMA2(t3, nh, b3);
 }
 
+// dft8v for inputs whose upper half v[4..7] is zero (a frame zero-padded to twice its length,
+// STOI's 256-sample window in a 512-point FFT): the first butterfly layer is the identity.
+// Same values as dft8v except for the sign of exact zeros (v + 0 there).
+__device__ __forceinline__ void dft8v_lo4(f2 v[8]) {
+  const f2 pm = {1.f, -1.f}, mp = {-1.f, 1.f};
+  const float h = 0.70710678118654752f;
+  const f2 hh = {h, h}, nh = {-h, -h};
+  const f2 b0 = v[0] + v[2], b2 = v[0] - v[2];
+  const f2 b1 = FSEM_FMA2(v[2].yx, pm, v[0]), b3 = FSEM_FMA2(v[2].yx, mp, v[0]);
+  const f2 c0 = v[1] + v[3], c2 = v[1] - v[3];
+  const f2 c1 = FSEM_FMA2(v[3].yx, pm, v[1]), c3 = FSEM_FMA2(v[3].yx, mp, v[1]);
+  const f2 t1 = FSEM_FMA2(c1.yx, pm, c1);
+  const f2 t3 = FSEM_FMA2(c3.yx, pm, -c3);
+  v[0] = b0 + c0;
+  v[4] = b0 - c0;
+  v[1] = FSEM_FMA2(t1, hh, b1);
+  v[5] = FSEM_FMA2(t1, nh, b1);
+  v[2] = FSEM_FMA2(c2.yx, pm, b2);
+  v[6] = FSEM_FMA2(c2.yx, mp, b2);
+  v[3] = FSEM_FMA2(t3, hh, b3);
+  v[7] = FSEM_FMA2(t3, nh, b3);
+}
+
 // 512-point complex FFT of one wave, radix-8 Stockham, natural-order result in
 // v[r] = Z[lane + 64 r].  `buf` = this wave's kFftBuf-float2 LDS exchange area.
+// LO4: Z[n] = 0 for n >= 256 (vc[4..7] are not read).
+template <bool LO4 = false>
 __device__ __forceinline__ void fft512_wave(cf vc[8], float2 *buf, int lane, const cf tw1[8],
                                             const cf tw2[8]) {
   f2 v[8];
 #pragma unroll
   for (int r = 0; r < 8; ++r) v[r] = (f2){vc[r].r, vc[r].i};
-  dft8v(v);
+  if (LO4)
+    dft8v_lo4(v);
+  else
+    dft8v(v);
 #pragma unroll
   for (int r = 0; r < 8; ++r) buf[fpad(8 * lane + r)] = make_float2(v[r].x, v[r].y);
   wave_lds_fence();

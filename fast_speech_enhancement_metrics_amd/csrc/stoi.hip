@@ -438,11 +438,12 @@ __global__ void __launch_bounds__(64 * TOB_WAVES)
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r].i = __builtin_amdgcn_ldexpf(v[r].i, sh);
     }
-    // wave-uniform factors (SGPR operands of the final multiply): 0.25 (x 2^-2k for the denoised
-    // power), or 0 for a zero frame
+    // wave-uniform factors, applied to the band sums (powers of two: the same values as scaling
+    // every bin, short of under/overflow): 0.25 (x 2^-2k for the denoised power), or 0 for a
+    // zero frame
     const float c_scale = c_zero ? 0.f : 0.25f;
     const float d_scale = d_zero ? 0.f : __builtin_amdgcn_ldexpf(0.25f, -2 * sh);
-    fft512_wave(v, wbuf, lane, tw1, tw2);
+    fft512_wave<true>(v, wbuf, lane, tw1, tw2);  // v[4..7] = 0: the frame's zero-padded half
     float pc[4], pd[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -453,8 +454,8 @@ __global__ void __launch_bounds__(64 * TOB_WAVES)
         mi = v[(8 - r) & 7].i;
       }
       const float zr = v[r].r, zi = v[r].i;
-      pc[r] = c_scale * fmaf(zr + mr, zr + mr, (zi - mi) * (zi - mi));  // explicit: no contraction choice
-      pd[r] = d_scale * fmaf(zi + mi, zi + mi, (zr - mr) * (zr - mr));
+      pc[r] = fmaf(zr + mr, zr + mr, (zi - mi) * (zi - mi));  // explicit: no contraction choice
+      pd[r] = fmaf(zi + mi, zi + mi, (zr - mr) * (zr - mr));
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -478,7 +479,8 @@ __global__ void __launch_bounds__(64 * TOB_WAVES)
       }
       // hardware square root (1 ulp; the correctly rounded sqrtf is a ~17-instruction sequence
       // that every lane of the wave issues)
-      if (pc_head) tob[((b + pc_sig * B) * NB + pc_band) * tmax + k] = __builtin_amdgcn_sqrtf(acc);
+      if (pc_head)
+        tob[((b + pc_sig * B) * NB + pc_band) * tmax + k] = __builtin_amdgcn_sqrtf(acc * (pc_sig ? d_scale : c_scale));
     }
     wave_lds_fence();
   }
