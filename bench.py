@@ -90,6 +90,34 @@ def cpu_baseline(clean, noisy, budget_s):
                       f"oracle numpy/C restatement, {dt:.1f} s"}
 
 
+def cpu_mode(clean, noisy, calls=5, batch=4):
+    """Informational: the package's own use_gpu=False path -- the reference's CPU mode restated in
+    torch/scipy (_cpu.py) -- on `batch` pairs of the workload with torch's default thread pool,
+    median of `calls` calls; not the contract's cpu_baseline (the oracle)."""
+    from fast_speech_enhancement_metrics_amd import PESQ_STOI
+    c, d = clean[:batch].cpu(), noisy[:batch].cpu()
+    m = PESQ_STOI(16000, use_gpu=False)
+    prev = torch.get_num_threads()
+    # the host's CPU share: OMP_NUM_THREADS where the launcher sets it (16 per GPU on the MI355X
+    # boxes), else every core
+    threads = max(1, int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    try:
+        m.scores(c, d)  # warm-up
+        ts = []
+        for _ in range(calls):
+            t0 = time.perf_counter()
+            m.scores(c, d)
+            ts.append(time.perf_counter() - t0)
+    finally:
+        torch.set_num_threads(prev)
+    ts.sort()
+    med = ts[len(ts) // 2]
+    return {"value": batch / med, "unit": "utterances/s", "cores": threads,
+            "sample": f"use_gpu=False path (torch/scipy), {batch} pairs x {clean.shape[1]} samples, "
+                      f"median of {calls} calls ({med * 1e3:.0f} ms)"}
+
+
 def kernel_roofline(clean, noisy, reps, joint):
     """HIP-event timing of the dominant kernel -- pesq_front, launched alone through its stage
     entry (fsem_pesq_front_y10_f32 for the joint path, fsem_pesq_front_f32 otherwise) -- on the
@@ -404,8 +432,9 @@ def main():
 
     out = None
     if rank == 0:
-        cpu = None
+        cpu = cpu_m = None
         if not args.no_cpu_baseline and world == 1:
+            cpu_m = cpu_mode(clean, noisy)
             cpu = cpu_baseline(clean, noisy, args.cpu_seconds)
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "utterances/s", "n_gpus": world,
@@ -417,7 +446,7 @@ def main():
                                        "fused joint entry PESQ_STOI.scores (one read of the inputs)")),
                        "batch_per_gpu": B, "global_batch": world * B, "length": L, "sample_rate": 16000,
                        "parallelism": f"dp{world} (utterance shards, RCCL all-gather of scores)"},
-            "roofline": roof, "cpu_baseline": cpu,
+            "roofline": roof, "cpu_baseline": cpu, "cpu_mode": cpu_m,
         }
         print(json.dumps(out), flush=True)
     if distributed:

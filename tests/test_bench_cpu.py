@@ -44,3 +44,10 @@ def test_roofline_traffic_from_newest_pmc_summary():
     newest = [r for r in rounds if os.path.exists(os.path.join(REPO, "profiles", r, "pmc_summary.json"))][-1]
     assert src == os.path.join("profiles", newest, "pmc_summary.json")
     assert bench.pmc_traffic("pesq_front<true, false>", 64, 160000) == (None, None)  # other sizes: none
+
+
+def test_cpu_mode_fields():
+    from fast_speech_enhancement_metrics_amd.synthetic import speech_like_pairs
+    c, n, _ = speech_like_pairs(2, 16000, 16000, seed=4)
+    out = bench.cpu_mode(c, n, calls=1, batch=2)
+    assert set(out) == {"value", "unit", "cores", "sample"} and out["value"] > 0
