@@ -485,7 +485,9 @@ __global__ void __launch_bounds__(PT, 2)
       const int band = 16 * t + (lane & 15);
       blo[t] = band < NBARK ? kBandEdge[band] : 0;
       bhi[t] = band < NBARK ? kBandEdge[band + 1] : 0;
-      bcor_c[t] = __float_as_uint(band < NBARK ? kBarkCorr[band] : 0.f);
+      // x 0.25: the Hermitian split's 1/4 (exact power of two, so the same products as scaling
+      // every bin before the GEMM, short of underflow)
+      bcor_c[t] = __float_as_uint(band < NBARK ? 0.25f * kBarkCorr[band] : 0.f);
     }
     auto in = [&](int t, int k) {
       const int bin = 4 * k + (lane >> 4);
@@ -686,8 +688,9 @@ __global__ void __launch_bounds__(PT, 2)
             mi = v[(8 - r) & 7].i;
           }
           const float zr = v[r].r, zi = v[r].i;
-          pa[r] = 0.25f * fmaf(zr + mr, zr + mr, (zi - mi) * (zi - mi));  // explicit: no contraction choice
-          pb[r] = 0.25f * fmaf(zi + mi, zi + mi, (zr - mr) * (zr - mr));
+          // 4 |Z_a|^2, 4 |Z_b|^2: the 1/4 is folded into the Bark weights (bcor)
+          pa[r] = fmaf(zr + mr, zr + mr, (zi - mi) * (zi - mi));  // explicit: no contraction choice
+          pb[r] = fmaf(zi + mi, zi + mi, (zr - mr) * (zr - mr));
         }
         if (lane == 0) {  // spec[:, :, 0] = 0 (PESQ.py:136)
           pa[0] = 0.f;
