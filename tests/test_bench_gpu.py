@@ -1,0 +1,37 @@
+"""bench.py end to end on the GPU at a small size (the driver's contract: one JSON line on stdout
+with the metric, throughput, roofline of the dominant kernel and the CPU legs), run as a child
+process like the driver runs it."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+REPO = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+
+
+def test_bench_json_line_contract():
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--batch", "64", "--length", "48000",
+                          "--steps", "2", "--warmup", "1", "--kernel-reps", "2", "--cpu-seconds", "0.5"],
+                         cwd=REPO, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, out.stdout  # the result line is the only line on stdout
+    d = json.loads(lines[0])
+    with open(os.path.join(REPO, "BASELINE.json")) as f:
+        assert d["metric"] == json.load(f)["metric"]
+    for key in ("value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+                "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline", "cpu_mode"):
+        assert key in d, key
+    assert d["n_gpus"] == 1 and d["steps"] == 2 and d["warmup"] == 1 and d["higher_is_better"] is True
+    assert d["value"] > 0 and abs(d["value"] - 64 * 1e3 / d["ms_per_step"]) < 1e-2 * d["value"]
+    r = d["roofline"]
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
+    assert r["algorithmic_bytes_per_launch"] == 2 * 64 * 48000 * 4
+    assert 0 < r["frac"] < 1 and abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
+    assert r["traffic"] is None  # PMC traffic is only recorded at the bench configuration
+    c = d["cpu_baseline"]
+    assert c["kind"] == "port" and c["cores"] == 1 and c["value"] > 0
+    assert d["cpu_mode"]["value"] > 0
