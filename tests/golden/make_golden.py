@@ -127,7 +127,37 @@ def varlen_case(name: str, lengths, sr: int, seed: int):
     print(name, out["pesq"], out["stoi"], out["estoi"])
 
 
+def tones_case(name: str, sr: int = 10000, length: int = 30000):
+    """Sinusoid pairs (nearly constant 1/3-octave envelope rows: the ill-conditioned case of the
+    segment statistics).  The reference runs twice, with torch seeds 0 and 1: the spread of its own
+    `1e-12 * randn` (STOI.py:116) and float32 rounding bounds what parity can mean here."""
+    import warnings
+    rng = np.random.default_rng(7)
+    t = np.arange(length) / float(sr)
+    c, d = [], []
+    for f in (250.0, 1000.0, 3150.0):
+        tone = 0.5 * np.sin(2 * np.pi * f * t)
+        c += [tone, tone + 0.025 * rng.standard_normal(length)]
+        d += [tone + 5e-4 * rng.standard_normal(length), tone]
+    codes_c = np.clip(np.round(np.stack(c) * 32768), -32768, 32767).astype(np.int16)
+    codes_d = np.clip(np.round(np.stack(d) * 32768), -32768, 32767).astype(np.int16)
+    clean = torch.from_numpy(codes_c.astype(np.float32) / 32768.0)
+    noisy = torch.from_numpy(codes_d.astype(np.float32) / 32768.0)
+    st = RefSTOI(sample_rate=sr, use_gpu=False)
+    out = dict(clean=codes_c, noisy=codes_d, sample_rate=sr)
+    for seed, suffix in ((0, ""), (1, "_seed1")):
+        torch.manual_seed(seed)
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            res = st(clean, noisy)
+        out["stoi" + suffix] = np.array([r["STOI"] for r in res])
+        out["estoi" + suffix] = np.array([r["ESTOI"] for r in res])
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
+    print(name, out["stoi"], out["estoi"], out["stoi_seed1"] - out["stoi"], out["estoi_seed1"] - out["estoi"])
+
+
 CASES = {
+    "tones_10k": lambda: tones_case("tones_10k"),
     "rate_8k": lambda: rate_case("rate_8k", batch=3, length=24000, sr=8000, seed=11),
     "varlen_16k": lambda: varlen_case("varlen_16k", [48000, 33333, 20001, 40960, 5000, 27003], sr=16000, seed=12),
     "varlen_8k": lambda: varlen_case("varlen_8k", [24000, 16667, 11111], sr=8000, seed=13),

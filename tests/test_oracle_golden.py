@@ -6,6 +6,7 @@ reference's own fast_se_metrics.PESQ / STOI (torchaudio restated, see oracle/ta_
 import numpy as np
 
 from oracle import pesq_oracle, stoi_oracle, ta
+from tests.conftest import load_golden
 
 
 def test_oracle_pesq_matches_reference(pesq_golden):
@@ -58,3 +59,16 @@ def test_resample_kernel_shape():
     assert (orig, new, width) == (8, 5, 10) and k.shape == (5, 28)
     k2, w2, o2, n2 = ta.sinc_resample_kernel(8000, 16000)
     assert (o2, n2) == (1, 2) and k2.shape == (2, 2 * w2 + 1)
+
+
+def test_oracle_stoi_tones_within_reference_conditioning():
+    """Sinusoid pairs (golden `tones_10k`, the reference run with torch seeds 0 and 1): nearly
+    constant 1/3-octave envelope rows make the segment statistics ill-conditioned, so the
+    reference's own float32 rounding -- not its `1e-12 * randn` (seed-to-seed spread <= 2e-9) --
+    sets how far any restatement can sit from it.  The oracle's float64 segment math is within
+    3.6e-4 (STOI) / 7.4e-4 (ESTOI) of it; BASELINE.json's parity target is 0.01."""
+    g = load_golden("tones_10k")
+    assert np.max(np.abs(g["stoi_seed1"] - g["stoi"])) < 1e-8 and np.max(np.abs(g["estoi_seed1"] - g["estoi"])) < 1e-8
+    s, e = stoi_oracle.stoi(g["clean_f"], g["noisy_f"], int(g["sample_rate"]))
+    np.testing.assert_allclose(s, g["stoi"], atol=1e-3, rtol=0)
+    np.testing.assert_allclose(e, g["estoi"], atol=1.5e-3, rtol=0)
