@@ -3,6 +3,7 @@
 Only the hot-path metrics (PESQ-wb, STOI/ESTOI) are provided; SDR, LSD, DNSMOS and
 SpeechBERTScore of the reference are out of scope.
 """
-from fast_speech_enhancement_metrics_amd import PESQ, STOI  # noqa: F401
+from fast_se_metrics.PESQ import PESQ  # noqa: F401  (module path first, then the class, as the reference)
+from fast_se_metrics.STOI import STOI  # noqa: F401
 
 __all__ = ["STOI", "PESQ"]

@@ -10,7 +10,10 @@ from __future__ import annotations
 import torch
 
 from . import _cpu, _native
+from .bark import BarkFilterBank
 from .base import BaseMetric, as_rows, check_row_rate, device_lengths, noisy_shape, resample_rows
+from .loudness import Loudness
+from .spectrogram import Spectrogram
 
 
 class PESQ(BaseMetric):
@@ -28,8 +31,8 @@ class PESQ(BaseMetric):
         return clean_speech / m, noisy_speech / m
 
     # ------------------------------------------------------------------ reference attributes
-    # The reference's filter coefficients (PESQ.py:79-90), float32 on the metric's device, built
-    # on first access (the engine carries its own copies in constant memory).
+    # The reference's constructor attributes (PESQ.py:63-90), on the metric's device, built on
+    # first access (the engine carries its own copies in constant memory).
     @property
     def power_filter(self) -> torch.Tensor:
         """[2, 11] (b; a) of the order-5 Butterworth band-pass 325-3250 Hz at 16 kHz (PESQ.py:80-81)."""
@@ -54,6 +57,143 @@ class PESQ(BaseMetric):
         if getattr(self, "_taper_weights", None) is None:
             self._taper_weights = torch.linspace(0, 15, 16, device=self.device)[1:] / 16.0
         return self._taper_weights
+
+    @property
+    def to_spec(self) -> Spectrogram:
+        """Hann-512 / hop-256 power spectrogram, center=False (PESQ.py:63-71)."""
+        if getattr(self, "_to_spec", None) is None:
+            self._to_spec = Spectrogram(win_length=512, n_fft=512, hop_length=256, window_fn=torch.hann_window,
+                                        power=2, normalized=False, center=False).to(self.device)
+        return self._to_spec
+
+    @property
+    def filter_bank(self) -> BarkFilterBank:
+        """P.862 Bark filterbank, 256 bins -> 49 bands (PESQ.py:74)."""
+        if getattr(self, "_filter_bank", None) is None:
+            self._filter_bank = BarkFilterBank(256, 49, device=self.device)
+        return self._filter_bank
+
+    @property
+    def loudness(self) -> Loudness:
+        """Zwicker loudness model over the 49 bands (PESQ.py:77)."""
+        if getattr(self, "_loudness", None) is None:
+            self._loudness = Loudness(49, device=self.device)
+        return self._loudness
+
+    # ------------------------------------------------------------------ stage methods
+    # The reference's pipeline stages (PESQ.py:92-230) on [rows, samples] tensors of 16 kHz
+    # speech.  On the GPU the band-pass power and the Bark bands come from the engine's front end
+    # (fsem_pesq_front_f32) and the disturbances from its back end (fsem_pesq_distances_f32); the
+    # remaining stages are short torch expressions on the metric's device.  Scores do not go
+    # through these methods: compute_metric runs the whole engine in one call.
+    def _front(self, speech: torch.Tensor):
+        """Engine front end on any number of rows -> (unscaled Bark bands [N, F, 49] float32,
+        sum of the squared band-pass output [N] float32)."""
+        x = as_rows(speech)
+        N, L = x.shape
+        if L % 4 or N % 2:
+            x = torch.nn.functional.pad(x, (0, (-L) % 4))
+            if N % 2:
+                x = torch.cat([x, x[-1:]], 0)  # the front end takes rows in (ref, deg) halves
+            x = x.contiguous()
+        h = x.shape[0] // 2
+        lib = _native.load()
+        F = lib.fsem_pesq_frames(L)
+        if F < 1:
+            raise RuntimeError("PESQ input shorter than one 512-sample frame")
+        fld = (F + 31) // 32 * 32
+        bark = torch.empty(2 * h, 49, fld, device=x.device)
+        power = torch.empty(2 * h, device=x.device)
+        ws = _native.workspace(lib.fsem_pesq_front_workspace_bytes(h, L), x.device)
+        _native.check(lib.fsem_pesq_front_f32(x[:h].data_ptr(), x[h:].data_ptr(), h, L, x.stride(0), None,
+                                              bark.data_ptr(), power.data_ptr(), ws.data_ptr(), ws.numel(),
+                                              _native.stream_handle(x.device)), "PESQ front")
+        return bark[:N, :, :F].transpose(1, 2), power[:N]
+
+    def align_level(self, speech: torch.Tensor) -> torch.Tensor:
+        """Rows scaled to band-pass power 1e7 (PESQ.py:92-102): x * sqrt(1e7 / P) with
+        P = sum(bandpass(x)^2) / (L + 5120) / 1.04684."""
+        speech = torch.atleast_2d(speech)
+        L = speech.shape[1]
+        if speech.is_cuda:
+            p = self._front(speech)[1].double()
+        else:
+            p = torch.from_numpy(_cpu.bandpass_power(speech.detach().to(torch.float64).numpy()))
+        gain = _cpu.level_scale(p, L).sqrt().to(speech.device, speech.dtype)
+        return speech * gain[:, None]
+
+    def pre_emphasize(self, speech: torch.Tensor) -> torch.Tensor:
+        """Edge taper (in place on ``speech``, as the reference) and the pre-emphasis IIR
+        (PESQ.py:104-113)."""
+        w = self.taper_weights.to(speech.device, speech.dtype)
+        speech[:, :15] *= w
+        speech[:, -15:] *= torch.flip(w, dims=(0,))
+        from scipy.signal import lfilter
+        y = lfilter(_cpu._PRE_B, _cpu._PRE_A, speech.detach().to("cpu", torch.float64).numpy(), axis=1)
+        return torch.from_numpy(y).to(speech.device, speech.dtype)
+
+    def get_bark_bands(self, speech: torch.Tensor) -> torch.Tensor:
+        """[N, L] rows -> [N, F, 49] float64 Bark power bands after level alignment and
+        pre-emphasis (PESQ.py:123-140)."""
+        speech = torch.atleast_2d(speech)
+        if not speech.is_cuda:
+            return _cpu.bark_of_rows(speech).to(speech.device)
+        bark, p = self._front(speech)
+        return bark.double() * _cpu.level_scale(p.double(), speech.shape[1])[:, None, None]
+
+    def equalize_bark_bands(self, clean_bark_bands: torch.Tensor, noisy_bark_bands: torch.Tensor):
+        """(clean, noisy) Bark bands after the band and frame power equalisation (PESQ.py:142-166)."""
+        return _cpu.equalize(clean_bark_bands, noisy_bark_bands)
+
+    def get_overlapping_sums(self, disturbance: torch.Tensor) -> torch.Tensor:
+        """[B, F] -> [B]: L6 over 20-frame windows (hop 10), then L2 over windows (PESQ.py:168-172)."""
+        return _cpu.overlapping_sums(disturbance)
+
+    def get_disturbances(self, clean_speech: torch.Tensor, noisy_speech: torch.Tensor):
+        """(symmetric, asymmetric) distances [B] of 16 kHz pairs (PESQ.py:174-230); MOS =
+        0.999 + 4 / (1 + exp(-1.3669 (4.5 - 0.1 sym - 0.0309 asym) + 3.8224))."""
+        clean = as_rows(clean_speech)
+        noisy = as_rows(noisy_speech)
+        if clean.shape != noisy.shape:
+            raise Exception("`clean_speech` and `denoised_speech` should have the same shape.")
+        if not clean.is_cuda:
+            return _cpu.pesq_distances(clean, noisy)
+        sym, asym, _ = self.frame_disturbances(clean, noisy)
+        return sym, asym
+
+    def frame_disturbances(self, clean_speech: torch.Tensor, noisy_speech: torch.Tensor, lengths=None):
+        """Engine back-end intermediates of 16 kHz pairs: (symmetric distance [B], asymmetric
+        distance [B], per-frame disturbances [B, 2, F] -- symmetric then asymmetric, after the
+        frame weighting and the clamp at 45, PESQ.py:222-224).  GPU only (the stage entry
+        fsem_pesq_distances_f32); rows under 20 frames give NaN distances."""
+        clean = as_rows(clean_speech)
+        noisy = as_rows(noisy_speech)
+        lib = _native.load()
+        B, L = clean.shape
+        F = lib.fsem_pesq_frames(L)
+        lens = device_lengths(lengths, B, L, clean.device) if lengths is not None else None
+        if F < 20 and lens is None:
+            raise RuntimeError(f"maximum size for tensor at dimension 1 is {max(F, 0)} but size is 20")
+        if clean.stride(0) != noisy.stride(0) or L % 4:
+            pad = (-L) % 4
+            clean = torch.nn.functional.pad(clean, (0, pad)).contiguous()
+            noisy = torch.nn.functional.pad(noisy, (0, pad)).contiguous()
+        fld = (F + 31) // 32 * 32
+        bark = torch.empty(2 * B, 49, fld, device=clean.device)
+        power = torch.empty(2 * B, device=clean.device)
+        st = _native.stream_handle(clean.device)
+        ws = _native.workspace(max(lib.fsem_pesq_front_workspace_bytes(B, L),
+                                   lib.fsem_pesq_distances_workspace_bytes(B, L)), clean.device)
+        lp = lens.data_ptr() if lens is not None else None
+        _native.check(lib.fsem_pesq_front_f32(clean.data_ptr(), noisy.data_ptr(), B, L, clean.stride(0), lp,
+                                              bark.data_ptr(), power.data_ptr(), ws.data_ptr(), ws.numel(), st),
+                      "PESQ front")
+        dist = torch.empty(2, B, device=clean.device)
+        frames = torch.full((B, 2, F), float("nan"), device=clean.device)
+        _native.check(lib.fsem_pesq_distances_f32(bark.data_ptr(), power.data_ptr(), B, L, lp, dist.data_ptr(),
+                                                  frames.data_ptr(), ws.data_ptr(), ws.numel(), st),
+                      "PESQ distances")
+        return dist[0], dist[1], frames
 
     # ------------------------------------------------------------------ device paths
     def scores(self, clean_speech: torch.Tensor, denoised_speech: torch.Tensor, lengths=None,

@@ -36,10 +36,11 @@ class STOI(BaseMetric):
     def normalize(x: torch.Tensor, dim: int = 0) -> torch.Tensor:
         """In place, as STOI.py:113-119: centre along ``dim`` and divide by the L2 norm.  Without the
         reference's ``1e-12 * randn`` term (deterministic, as the engine): a zero-variance slice
-        becomes 0 instead of a random unit vector."""
+        becomes 0 instead of a random unit vector.  Non-finite slices stay non-finite (NaN / Inf
+        propagate as in the reference)."""
         x -= x.mean(dim=dim, keepdim=True)
         n = torch.linalg.vector_norm(x, ord=2, dim=dim, keepdim=True)
-        x.copy_(torch.where(n > 0, x / torch.where(n > 0, n, torch.ones_like(n)), torch.zeros_like(x)))
+        x.copy_(torch.where(n == 0, torch.zeros_like(x), x / torch.where(n == 0, torch.ones_like(n), n)))
         return x
 
     # ------------------------------------------------------------------ reference attributes
@@ -62,6 +63,88 @@ class STOI(BaseMetric):
         if getattr(self, "_window", None) is None:
             self._window = torch.hann_window(self.win_length + 1, dtype=torch.float32, device=self.device)[1:]
         return self._window
+
+    # ------------------------------------------------------------------ stage methods
+    # The reference's pipeline stages (STOI.py:49-198) on 10 kHz tensors, as torch expressions on
+    # the metric's device (the overlap-add without the reference's per-utterance Python loop).
+    # Scores do not go through these: on the GPU compute_metric runs the whole engine
+    # (fsem_stoi_f32), which never materialises the overlap-added signal or the [B, S, 15, 30]
+    # segments.
+    def stft(self, speech: torch.Tensor, lengths: torch.Tensor) -> torch.Tensor:
+        """[N, T] -> [N, 257, frames] power spectrogram (n_fft 512, the 256-sample window centred,
+        hop 128, center=False); frames at or past 1 + (length - 512) // 128 are zeroed (STOI.py:49-69)."""
+        spec = torch.stft(speech, n_fft=self.n_fft, hop_length=self.hop_length, win_length=self.win_length,
+                          window=self.window.to(speech.device, speech.dtype), center=False, normalized=False,
+                          return_complex=True, onesided=True).abs().square()
+        n_valid = 1 + (lengths.to(spec.device) - self.n_fft) // self.hop_length
+        t = torch.arange(spec.shape[-1], device=spec.device)
+        return spec.masked_fill((t[None, :] >= n_valid[:, None])[:, None, :], 0)
+
+    def overlap_and_add(self, frames: torch.Tensor, lengths: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+        """Kept frames [sum(lengths), 256] of B utterances (``lengths`` frames each, in order) ->
+        (signals [B, max_len], (lengths + 1) * 128): frame j of utterance b added at 128 j
+        (STOI.py:71-86)."""
+        lengths = lengths.to(frames.device)
+        out_len = (lengths + 1) * self.hop_length
+        B = lengths.numel()
+        width = int(out_len.max().item()) if B else 0
+        sig = torch.zeros(B, width, dtype=frames.dtype, device=frames.device)
+        if frames.numel():
+            utt = torch.repeat_interleave(torch.arange(B, device=frames.device), lengths)
+            first = torch.cumsum(lengths, 0) - lengths  # index of each utterance's first frame
+            j = torch.arange(frames.shape[0], device=frames.device) - first[utt]
+            pos = (utt * width + self.hop_length * j)[:, None] + torch.arange(self.win_length, device=frames.device)
+            sig.view(-1).index_add_(0, pos.reshape(-1), frames.reshape(-1))
+        return sig, out_len
+
+    def remove_silent_frames(self, clean_speech: torch.Tensor, denoised_speech: torch.Tensor):
+        """Frames (256, hop 128, windowed) more than 40 dB below the clean signal's loudest frame are
+        dropped from both signals, which are rebuilt by overlap-add -> (clean, denoised, lengths)
+        (STOI.py:88-111)."""
+        w = self.window.to(clean_speech.device, clean_speech.dtype)
+        cf = clean_speech.unfold(1, self.win_length, self.hop_length) * w
+        df = denoised_speech.unfold(1, self.win_length, self.hop_length) * w
+        energy = 20 * torch.log10(torch.linalg.vector_norm(cf, dim=2) + 1e-9)
+        keep = (energy.amax(dim=1, keepdim=True) - self.dynamic_range - energy) < 0
+        n = keep.sum(1)
+        c, lens = self.overlap_and_add(cf[keep], n)
+        d, _ = self.overlap_and_add(df[keep], n)
+        return c, d, lens
+
+    def compute_segments(self, speech: torch.Tensor, lengths: torch.Tensor):
+        """1/3-octave band envelopes sqrt(OBM . |STFT|^2) [N, 15, T] cut into the T - 29 sliding
+        30-frame windows (views) (STOI.py:121-127)."""
+        obm = self.octave_band_matrix.to(speech.device, speech.dtype)
+        tob = torch.sqrt(torch.matmul(obm, self.stft(speech, lengths)))
+        return [tob[:, :, m:m + self.N] for m in range(max(tob.shape[2] - self.N + 1, 0))]
+
+    def equalize_clip(self, clean_segments: torch.Tensor, denoised_segments: torch.Tensor) -> torch.Tensor:
+        """Denoised segments scaled to the clean segments' norm over the 30 frames, then clipped at
+        (1 + 10^(-beta/20)) x clean (STOI.py:129-139)."""
+        nc = torch.linalg.vector_norm(clean_segments, dim=3, keepdim=True)
+        nd = torch.linalg.vector_norm(denoised_segments, dim=3, keepdim=True)
+        bound = clean_segments * (1 + 10 ** (-self.beta / 20))
+        return torch.minimum(denoised_segments * (nc / (nd + 1e-9)), bound)
+
+    def compute_correlation(self, clean_segments: torch.Tensor, denoised_segments: torch.Tensor,
+                            mask: torch.Tensor, extended: bool) -> torch.Tensor:
+        """Masked sum over (segment, band, frame) of the products, / 30 (ESTOI) or / 15 (STOI)
+        (STOI.py:141-151)."""
+        prod = denoised_segments * clean_segments * mask[:, :, None, None]
+        return prod.sum(dim=(1, 2, 3)) / (self.N if extended else self.num_octave_bands)
+
+    @torch.no_grad()
+    def compute_stoi(self, clean_speech: torch.Tensor, denoised_speech: torch.Tensor):
+        """(stoi [B], estoi [B]) of 10 kHz signals (STOI.py:153-198); with no 30-frame segment in
+        the batch, the reference's warning and (tensor(0), tensor(0)).  GPU: the engine."""
+        if clean_speech.is_cuda:
+            s, e = self.scores(clean_speech, denoised_speech, self.EXPECTED_SAMPLING_RATE)
+        else:
+            s, e = _cpu.stoi(torch.atleast_2d(clean_speech), torch.atleast_2d(denoised_speech))
+        if bool(torch.isnan(s).all()):
+            warnings.warn("Not enough non-silent frames. Please check your sound files", RuntimeWarning, stacklevel=2)
+            return torch.tensor(0), torch.tensor(0)
+        return s, e
 
     def scores(self, clean_speech: torch.Tensor, denoised_speech: torch.Tensor, sample_rate: int | None = None,
                lengths=None):

@@ -45,60 +45,116 @@ def pesq_frames(L: int) -> int:
     return 0 if Lp < 512 else 1 + (Lp - 512) // 256
 
 
-def pesq(clean: torch.Tensor, noisy: torch.Tensor) -> torch.Tensor:
-    """[B, L] 16 kHz float32 -> MOS [B] float64."""
+def bandpass_power(x: np.ndarray) -> np.ndarray:
+    """[N, L] -> [N] sum of the squared band-pass output (PESQ.py:94-97, before / (L+5120) / 1.04684)."""
+    y = sosfilt(_BP_SOS, x, axis=1)
+    return (y * y).sum(axis=1)
+
+
+def level_scale(power_sum, L: int):
+    """1e7 / (power / (L + 5120) / 1.04684): the factor on a row's power (PESQ.py:97-100)."""
+    return 1e7 / (power_sum / (L + 5120) / 1.04684)
+
+
+def pre_emphasize(x: np.ndarray) -> np.ndarray:
+    """Edge taper (k/16 on the first and last 15 samples) + the pre-emphasis IIR (PESQ.py:104-113),
+    on a copy."""
+    x = np.array(x, dtype=np.float64)
+    x[:, :15] *= _TAPER.numpy()
+    x[:, -15:] *= _TAPER.numpy()[::-1]
+    return lfilter(_PRE_B, _PRE_A, x, axis=1)
+
+
+def power_spectrum(x: torch.Tensor) -> torch.Tensor:
+    """[N, L] -> [N, F, 257]: pad by L % 256 (PESQ.py:128-130), Hann-512 / hop-256 |rFFT|^2, the
+    DC bin zeroed (PESQ.py:133-136)."""
+    pad = x.shape[1] % 256
+    if pad:
+        x = torch.nn.functional.pad(x, (0, pad))
+    spec = torch.stft(x, n_fft=512, hop_length=256, win_length=512,
+                      window=torch.hann_window(512, dtype=x.dtype, device=x.device),
+                      center=False, return_complex=True).abs().square().transpose(1, 2)
+    spec[:, :, 0] = 0.0
+    return spec
+
+
+def bark_bands(spec: torch.Tensor) -> torch.Tensor:
+    """[N, F, 257] -> [N, F, 49] (bark.py:203-204)."""
+    return torch.einsum("ij,klj->kli", _FBANK.to(spec.device), spec[:, :, :-1]) * _CORR.to(spec.device)
+
+
+def bark_of_rows(x: torch.Tensor) -> torch.Tensor:
+    """PESQ.get_bark_bands on [N, L] rows: level alignment, pre-emphasis, spectrum, Bark bands."""
+    L = x.shape[1]
+    xd = x.detach().to("cpu", torch.float64).numpy()
+    xd = xd * np.sqrt(level_scale(bandpass_power(xd), L))[:, None]
+    return bark_bands(power_spectrum(torch.from_numpy(pre_emphasize(xd))))
+
+
+def equalize(c: torch.Tensor, n: torch.Tensor):
+    """PESQ.equalize_bark_bands (PESQ.py:142-166) -> (equalised clean, equalised noisy)."""
+    thr = _THR.to(c.device)
+    silent = (c * (c > thr * 100.0)).sum(2) < 1e7
+    keep = (~silent).unsqueeze(-1)
+    mc = (c * ((c > thr * 100.0) & keep)).mean(1)
+    mn = (n * ((n > thr * 100.0) & keep)).mean(1)
+    ratio = ((mn + 1000.0) / (mc + 1000.0)).clamp(0.01, 100.0)
+    ec = ratio.unsqueeze(1) * c
+    fr = ((ec * (ec > thr)).sum(2) + 5e3) / ((n * (n > thr)).sum(2) + 5e3)
+    fr2 = fr.clone()
+    fr2[:, 1:] = 0.8 * fr[:, 1:] + 0.2 * fr[:, :-1]
+    return ec, fr2.clamp(3e-4, 5.0).unsqueeze(-1) * n
+
+
+def loudness(p: torch.Tensor) -> torch.Tensor:
+    thr, ex = _THR.to(p.device), _EXP.to(p.device)
+    v = (2.0 * thr) ** ex * ((0.5 + 0.5 * p / thr) ** ex - 1.0)
+    return torch.where(p <= thr, torch.zeros_like(v), v) * T.SL_16K
+
+
+def frame_disturbances(ec: torch.Tensor, en: torch.Tensor):
+    """Per-frame symmetric / asymmetric disturbances after the frame weighting and the clamp at 45
+    (PESQ.py:193-224) -> ([B, F], [B, F])."""
+    wb = _WB.to(ec.device)
+    lc, ln = loudness(ec), loudness(en)
+    d = ln - lc
+    d = d.sign() * (d.abs() - 0.25 * torch.minimum(lc, ln)).clamp(min=0)
+    sym = (math.sqrt(_TW) * torch.sqrt(((wb * d)[:, :, 1:] ** 2).sum(2))).clamp(min=1e-20)
+    a = ((en + 50.0) / (ec + 50.0)) ** 1.2
+    a = torch.where(a < 3.0, torch.zeros_like(a), a).clamp(max=12.0)
+    asym = (wb * d * a)[:, :, 1:].abs().sum(2).clamp(min=1e-20)
+    thr = _THR.to(ec.device)
+    w = (((ec * (ec > thr)).sum(2) + 1e5) / 1e7) ** 0.04
+    return (sym / w).clamp(max=45.0), (asym / w).clamp(max=45.0)
+
+
+def overlapping_sums(v: torch.Tensor) -> torch.Tensor:
+    """[B, F] -> [B]: L6 within 20-frame windows (hop 10), L2 across windows (PESQ.py:168-172)."""
+    fr_ = v.unfold(1, 20, 10)
+    return (fr_ ** 6).mean(2).pow(1.0 / 6.0).square().mean(1).sqrt()
+
+
+def mos_of(sd: torch.Tensor, ad: torch.Tensor) -> torch.Tensor:
+    """PESQ.py:240-243."""
+    m = 4.5 - 0.1 * sd - 0.0309 * ad
+    return 0.999 + 4.0 / (1.0 + torch.exp(-1.3669 * m + 3.8224))
+
+
+def pesq_distances(clean: torch.Tensor, noisy: torch.Tensor):
+    """PESQ.get_disturbances: [B, L] 16 kHz -> (symmetric, asymmetric) distances [B] float64."""
     B, L = clean.shape
     F = pesq_frames(L)
     if F < 20:
         raise RuntimeError(f"maximum size for tensor at dimension 1 is {max(F, 0)} but size is 20")
-    x = torch.cat([clean, noisy], 0).to(torch.float64).numpy()
-    y = sosfilt(_BP_SOS, x, axis=1)
-    power = (y * y).sum(axis=1) / (L + 5120) / 1.04684
-    x = x * np.sqrt(1e7 / power)[:, None]
-    x[:, :15] *= _TAPER.numpy()
-    x[:, -15:] *= _TAPER.numpy()[::-1]
-    x = lfilter(_PRE_B, _PRE_A, x, axis=1)
-    pad = L % 256
-    xt = torch.from_numpy(x)
-    if pad:
-        xt = torch.nn.functional.pad(xt, (0, pad))
-    spec = torch.stft(xt, n_fft=512, hop_length=256, win_length=512, window=torch.hann_window(512, dtype=torch.float64),
-                      center=False, return_complex=True).abs().square().transpose(1, 2)    # [2B, F, 257]
-    spec[:, :, 0] = 0.0
-    bark = torch.einsum("ij,klj->kli", _FBANK, spec[:, :, :-1]) * _CORR
-    c, n = bark[:B], bark[B:]
-    silent = (c * (c > _THR * 100.0)).sum(2) < 1e7
-    keep = (~silent).unsqueeze(-1)
-    mc = (c * ((c > _THR * 100.0) & keep)).mean(1)
-    mn = (n * ((n > _THR * 100.0) & keep)).mean(1)
-    ratio = ((mn + 1000.0) / (mc + 1000.0)).clamp(0.01, 100.0)
-    ec = ratio.unsqueeze(1) * c
-    fr = ((ec * (ec > _THR)).sum(2) + 5e3) / ((n * (n > _THR)).sum(2) + 5e3)
-    fr2 = fr.clone()
-    fr2[:, 1:] = 0.8 * fr[:, 1:] + 0.2 * fr[:, :-1]
-    en = fr2.clamp(3e-4, 5.0).unsqueeze(-1) * n
+    bark = bark_of_rows(torch.cat([clean, noisy], 0))
+    ec, en = equalize(bark[:B], bark[B:])
+    sym, asym = frame_disturbances(ec, en)
+    return overlapping_sums(sym), overlapping_sums(asym)
 
-    def loud(p):
-        v = (2.0 * _THR) ** _EXP * ((0.5 + 0.5 * p / _THR) ** _EXP - 1.0)
-        return torch.where(p <= _THR, torch.zeros_like(v), v) * T.SL_16K
 
-    lc, ln = loud(ec), loud(en)
-    d = ln - lc
-    d = d.sign() * (d.abs() - 0.25 * torch.minimum(lc, ln)).clamp(min=0)
-    sym = (math.sqrt(_TW) * torch.sqrt(((_WB * d)[:, :, 1:] ** 2).sum(2))).clamp(min=1e-20)
-    a = ((en + 50.0) / (ec + 50.0)) ** 1.2
-    a = torch.where(a < 3.0, torch.zeros_like(a), a).clamp(max=12.0)
-    asym = (_WB * d * a)[:, :, 1:].abs().sum(2).clamp(min=1e-20)
-    w = (((ec * (ec > _THR)).sum(2) + 1e5) / 1e7) ** 0.04
-    sym = (sym / w).clamp(max=45.0)
-    asym = (asym / w).clamp(max=45.0)
-
-    def pool(v):
-        fr_ = v.unfold(1, 20, 10)
-        return (fr_ ** 6).mean(2).pow(1.0 / 6.0).square().mean(1).sqrt()
-
-    m = 4.5 - 0.1 * pool(sym) - 0.0309 * pool(asym)
-    return 0.999 + 4.0 / (1.0 + torch.exp(-1.3669 * m + 3.8224))
+def pesq(clean: torch.Tensor, noisy: torch.Tensor) -> torch.Tensor:
+    """[B, L] 16 kHz float32 -> MOS [B] float64."""
+    return mos_of(*pesq_distances(clean, noisy))
 
 
 # ----------------------------------------------------------------------------- STOI

@@ -47,6 +47,8 @@ SIGNATURES = {
                                                 _vp, _c_i64, _vp, _c_sz, _vp]),
     "fsem_pesq_back_workspace_bytes": (_c_sz, [_c_i64, _c_i64]),
     "fsem_pesq_back_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _vp, _vp, _vp, _c_sz, _vp]),
+    "fsem_pesq_distances_workspace_bytes": (_c_sz, [_c_i64, _c_i64]),
+    "fsem_pesq_distances_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _c_sz, _vp]),
     "fsem_stoi_workspace_bytes": (_c_sz, [_c_i64, _c_i64, _c_i32]),
     "fsem_stoi_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _c_i32, _vp, _vp, _vp, _c_sz, _vp]),
     "fsem_stoi_tob_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_i64, _vp, _c_sz, _vp]),

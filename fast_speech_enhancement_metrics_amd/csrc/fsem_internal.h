@@ -24,7 +24,8 @@ int launch_front(const float *ref, const float *deg, int64_t batch, int64_t leng
 // pesq_back over bark with the signal powers given (power) or summed from the front end's
 // per-segment partials (ppart, power == nullptr); ws as fsem_pesq_back_workspace_bytes
 int launch_back(const float *bark, const float *power, const float *ppart, int64_t batch, int64_t length,
-                const int32_t *lengths, float *mos, void *ws, size_t ws_bytes, hipStream_t stream);
+                const int32_t *lengths, float *mos, void *ws, size_t ws_bytes, hipStream_t stream,
+                float *dist = nullptr, float *frames = nullptr);
 // the two halves of run_wb on one workspace (fsem_pesq_workspace_bytes): the front end (as
 // launch_front) and, once it is complete on back_st, the back end writing mos
 int run_wb_front(const float *ref, const float *deg, int64_t batch, int64_t length, int64_t ld,

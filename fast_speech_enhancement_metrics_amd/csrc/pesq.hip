@@ -853,18 +853,24 @@ __device__ __forceinline__ float loud(float p, int b) {
 // chip (no barriers, no idle waves at the end of an utterance: the throughput form); BW = 4 for
 // small batches, where one utterance's latency is the call's.  The two differ only in the
 // summation order of the band totals and of the window L2 sum (~1e-7 relative in the score).
-template <int BW>
+// STAGE: the stage entry's instance (fsem_pesq_distances_f32), which also writes the distances
+// and the per-frame disturbances; the scoring instances carry no trace of those outputs.
+template <int BW, bool STAGE = false>
 __global__ void __launch_bounds__(64 * BW) __attribute__((amdgpu_waves_per_eu(4)))
     pesq_back(const float *__restrict__ bark, const float *__restrict__ power, const float *__restrict__ ppart,
               int nseg, int64_t B, int64_t Lcap, const int32_t *__restrict__ lens, int Fcap,
-              float *__restrict__ scratch, float *__restrict__ mos) {
+              float *__restrict__ scratch, float *__restrict__ mos, float *__restrict__ dist,
+              float *__restrict__ frames) {
   constexpr int BT = 64 * BW;
   const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t b = blockIdx.x;
   const int64_t L = row_length(lens, b, Lcap);
   const int F = frames_of(L);  // this utterance's frames; rows are laid out with stride bark_ld(Fcap)
   if (F < 20) {  // the reference's unfold(1, 20, 10) raises here (PESQ.py:169)
-    if (tid == 0) mos[b] = __builtin_nanf("");
+    if (tid == 0) {
+      mos[b] = __builtin_nanf("");
+      if (STAGE && dist) dist[b] = dist[B + b] = __builtin_nanf("");
+    }
     return;
   }
   const int64_t fld = bark_ld(Fcap);
@@ -1051,8 +1057,13 @@ __global__ void __launch_bounds__(64 * BW) __attribute__((amdgpu_waves_per_eu(4)
     const float ay = fmaxf(as, 1e-20f);
     const float w = pow_pos((ac + 1e5f) / 1e7f, 0.04f);
     if (valid) {
-      sym[f] = fminf(sy / w, 45.f);
-      asym[f] = fminf(ay / w, 45.f);
+      const float fs_ = fminf(sy / w, 45.f), fa_ = fminf(ay / w, 45.f);
+      sym[f] = fs_;
+      asym[f] = fa_;
+      if (STAGE && frames) {  // stage entry only (fsem_pesq_distances_f32): [B, 2, Fcap]
+        frames[(2 * b) * (int64_t)Fcap + f] = fs_;
+        frames[(2 * b + 1) * (int64_t)Fcap + f] = fa_;
+      }
     }
   }
   __syncthreads();  // pass 3 reads other waves' sym / asym stores
@@ -1091,7 +1102,12 @@ __global__ void __launch_bounds__(64 * BW) __attribute__((amdgpu_waves_per_eu(4)
     // a signal with zero (or non-finite) band-pass power: the reference's x * sqrt(1e7 / power)
     // (PESQ.py:100) turns it into NaN samples, which torch's clamp / pow propagate to the score;
     // here the scale multiplies Bark bands whose NaNs the comparisons above would drop
-    mos[b] = (__builtin_isfinite(sc) && __builtin_isfinite(sn)) ? (float)m : __builtin_nanf("");
+    const bool fin = __builtin_isfinite(sc) && __builtin_isfinite(sn);
+    mos[b] = fin ? (float)m : __builtin_nanf("");
+    if (STAGE && dist) {  // stage entry only: the symmetric / asymmetric distances (PESQ.py:227-230)
+      dist[b] = fin ? (float)ds : __builtin_nanf("");
+      dist[B + b] = fin ? (float)da : __builtin_nanf("");
+    }
   }
 }
 
@@ -1211,7 +1227,7 @@ extern "C" size_t fsem_pesq_back_workspace_bytes(int64_t batch, int64_t length) 
 
 int fsem::pesq::launch_back(const float *bark, const float *power, const float *ppart, int64_t batch,
                             int64_t length, const int32_t *lengths, float *mos, void *ws, size_t ws_bytes,
-                            hipStream_t stream) {
+                            hipStream_t stream, float *dist, float *frames) {
   if (!bark || (!power && !ppart) || !mos || batch <= 0 || length <= 0 || length > kMaxLength) return FSEM_EINVAL;
   const pesq::Geometry g = pesq::geometry(length);
   if (g.F < 20 && !lengths) return FSEM_ESHORT;
@@ -1219,12 +1235,18 @@ int fsem::pesq::launch_back(const float *bark, const float *power, const float *
   if (batch > 0x7fffffff) return FSEM_EINVAL;
   const int bw = pesq::back_waves(batch, length);
   float *scratch = static_cast<float *>(ws);
-#define FSEM_BACK(W, LDS)                                                                                    \
-  hipLaunchKernelGGL(pesq::pesq_back<W>, dim3((unsigned)batch), dim3(64 * W), LDS, stream, bark, power, ppart, \
-                     g.nseg, batch, length, lengths, g.F, scratch, mos)
-  if (bw == 8) FSEM_BACK(8, 0);
-  else if (bw == 4) FSEM_BACK(4, 0);
-  else FSEM_BACK(1, pesq::back_keep_bytes(length));
+#define FSEM_BACK(W, S, LDS)                                                                                   \
+  hipLaunchKernelGGL((pesq::pesq_back<W, S>), dim3((unsigned)batch), dim3(64 * W), LDS, stream, bark, power, ppart, \
+                     g.nseg, batch, length, lengths, g.F, scratch, mos, dist, frames)
+  if (dist || frames) {
+    if (bw == 8) FSEM_BACK(8, true, 0);
+    else if (bw == 4) FSEM_BACK(4, true, 0);
+    else FSEM_BACK(1, true, pesq::back_keep_bytes(length));
+  } else {
+    if (bw == 8) FSEM_BACK(8, false, 0);
+    else if (bw == 4) FSEM_BACK(4, false, 0);
+    else FSEM_BACK(1, false, pesq::back_keep_bytes(length));
+  }
 #undef FSEM_BACK
   FSEM_CHECK_LAUNCH();
   return FSEM_OK;
@@ -1235,6 +1257,22 @@ extern "C" int fsem_pesq_back_f32(const float *bark, const float *power, int64_t
                                   void *stream) {
   if (!power) return FSEM_EINVAL;
   return pesq::launch_back(bark, power, nullptr, batch, length, lengths, mos, ws, ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" size_t fsem_pesq_distances_workspace_bytes(int64_t batch, int64_t length) {
+  // the back end's scratch rows, then the scores it also writes
+  return fsem_pesq_back_workspace_bytes(batch, length) + align_up(sizeof(float) * (size_t)batch, 256);
+}
+
+extern "C" int fsem_pesq_distances_f32(const float *bark, const float *power, int64_t batch, int64_t length,
+                                       const int32_t *lengths, float *dist, float *frames, void *ws,
+                                       size_t ws_bytes, void *stream) {
+  if (!power || !dist || batch <= 0 || length <= 0) return FSEM_EINVAL;
+  if (!ws || ws_bytes < fsem_pesq_distances_workspace_bytes(batch, length)) return FSEM_EWORKSPACE;
+  const size_t back = fsem_pesq_back_workspace_bytes(batch, length);
+  float *mos = reinterpret_cast<float *>(static_cast<char *>(ws) + back);
+  return pesq::launch_back(bark, power, nullptr, batch, length, lengths, mos, ws, back, (hipStream_t)stream, dist,
+                           frames);
 }
 
 hipStream_t fsem::side_stream(hipStream_t st) {
@@ -1254,14 +1292,30 @@ hipStream_t fsem::side_stream(hipStream_t st) {
   return side[dev];
 }
 
+namespace {
+// The join events of one host thread, one per device, released when the thread exits
+// (errors ignored: at process exit the runtime may already be gone).
+struct ThreadEvents {
+  static constexpr int kMaxDev = 64;
+  hipEvent_t ev[kMaxDev] = {};
+  ~ThreadEvents() {
+    for (hipEvent_t &e : ev)
+      if (e) (void)hipEventDestroy(e);
+  }
+};
+}  // namespace
+
 int fsem::stream_wait(hipStream_t waiter, hipStream_t producer) {
   if (waiter == producer) return FSEM_OK;
-  // one event per (host thread, device), recorded anew for every edge: a wait enqueued earlier
-  // keeps the record it was enqueued behind, and no other thread records this event
-  constexpr int kMaxDev = 64;
-  thread_local hipEvent_t ev[kMaxDev] = {};
+  // One event per (host thread, device), recorded anew for every edge.  This relies on the
+  // HIP (as CUDA) snapshot semantics of hipStreamWaitEvent: a wait waits for the record that is
+  // the event's most recent one WHEN THE WAIT IS ENQUEUED, so re-recording the event for the
+  // next edge (possibly on another stream) does not move an earlier wait.  No other thread
+  // records this event.
+  thread_local ThreadEvents tev;
+  hipEvent_t *ev = tev.ev;
   hipDevice_t dev = 0;
-  if (hipStreamGetDevice(producer, &dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return FSEM_ELAUNCH;
+  if (hipStreamGetDevice(producer, &dev) != hipSuccess || dev < 0 || dev >= ThreadEvents::kMaxDev) return FSEM_ELAUNCH;
   if (!ev[dev]) {
     int cur = 0;
     if (hipGetDevice(&cur) != hipSuccess) return FSEM_ELAUNCH;

@@ -438,11 +438,13 @@ __global__ void __launch_bounds__(64 * TOB_WAVES)
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r].i = __builtin_amdgcn_ldexpf(v[r].i, sh);
     }
-    // wave-uniform factors, applied to the band sums (powers of two: the same values as scaling
-    // every bin, short of under/overflow): 0.25 (x 2^-2k for the denoised power), or 0 for a
-    // zero frame
-    const float c_scale = c_zero ? 0.f : 0.25f;
-    const float d_scale = d_zero ? 0.f : __builtin_amdgcn_ldexpf(0.25f, -2 * sh);
+    // wave-uniform factors, applied to the band envelopes after the square root (powers of two:
+    // the same values as scaling every bin's power by 0.25 (x 2^-2sh for the denoised power),
+    // short of under/overflow), or 0 for a zero frame.  Scaling after the root keeps the
+    // hardware sqrt's input at the equalised level: v_sqrt_f32 loses accuracy on tiny and
+    // denormal inputs, which a quiet denoised frame scaled down first would feed it.
+    const float c_scale = c_zero ? 0.f : 0.5f;
+    const float d_scale = d_zero ? 0.f : __builtin_amdgcn_ldexpf(0.5f, -sh);
     fft512_wave<true>(v, wbuf, lane, tw1, tw2);  // v[4..7] = 0: the frame's zero-padded half
     float pc[4], pd[4];
 #pragma unroll
@@ -480,7 +482,7 @@ __global__ void __launch_bounds__(64 * TOB_WAVES)
       // hardware square root (1 ulp; the correctly rounded sqrtf is a ~17-instruction sequence
       // that every lane of the wave issues)
       if (pc_head)
-        tob[((b + pc_sig * B) * NB + pc_band) * tmax + k] = __builtin_amdgcn_sqrtf(acc * (pc_sig ? d_scale : c_scale));
+        tob[((b + pc_sig * B) * NB + pc_band) * tmax + k] = __builtin_amdgcn_sqrtf(acc) * (pc_sig ? d_scale : c_scale);
     }
     wave_lds_fence();
   }

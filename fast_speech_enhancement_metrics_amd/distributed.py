@@ -139,17 +139,27 @@ def scatter_batch(clean, noisy, src: int = 0, group=None, lengths=None, device=N
     rank = dist.get_rank(group)
     gsrc = dist.get_global_rank(group, src) if group is not None else src
     dev = collective_device(group, device if device is not None else (noisy.device if noisy is not None else None))
-    # shape, dtype code and whether lengths come along: one small broadcast
+    # shape, dtype code and whether lengths come along: one small broadcast.  A bad call is
+    # reported through the broadcast (code -1) so that every rank raises -- raising on `src`
+    # alone would leave the other ranks blocked in the broadcast.
     dtypes = [torch.float32, torch.float16, torch.bfloat16, torch.float64]
     meta = torch.zeros(4, dtype=torch.int64, device=dev)
     if rank == src:
-        if clean.shape != noisy.shape or clean.dim() != 2:
-            raise ValueError("scatter_batch: clean / noisy must be [B, L] of one shape")
-        meta[0], meta[1] = clean.shape[0], clean.shape[1]
-        meta[2] = dtypes.index(noisy.dtype)
-        meta[3] = 0 if lengths is None else 1
+        ok = (clean is not None and noisy is not None and clean.shape == noisy.shape and clean.dim() == 2)
+        if ok and (clean.dtype != noisy.dtype or noisy.dtype not in dtypes):
+            # one wire dtype for both signals: mixed or other dtypes (int16 codes, ...) go as the
+            # float32 the metrics compute in
+            clean, noisy = clean.to(torch.float32), noisy.to(torch.float32)
+        if ok:
+            meta[0], meta[1] = clean.shape[0], clean.shape[1]
+            meta[2] = dtypes.index(noisy.dtype)
+            meta[3] = 0 if lengths is None else 1
+        else:
+            meta[2] = -1
     dist.broadcast(meta, gsrc, group=group)
     B, L, code, has_len = (int(v) for v in meta.tolist())
+    if code < 0:
+        raise ValueError("scatter_batch: clean / noisy on the source rank must be [B, L] of one shape")
     dtype = dtypes[code]
     lens_all = torch.empty(B, dtype=torch.int64, device=dev)
     if has_len:

@@ -119,6 +119,18 @@ size_t fsem_pesq_back_workspace_bytes(int64_t batch, int64_t length);
 int fsem_pesq_back_f32(const float *bark, const float *power, int64_t batch, int64_t length,
                        const int32_t *lengths, float *mos, void *ws, size_t ws_bytes,
                        void *stream);
+/* distances: the back end's intermediates instead of the scores -- replaces
+ *        PESQ.get_disturbances (PESQ.py:174-230) on the front end's tensors:
+ *          dist   [2, batch] float32: symmetric distance (row 0) and asymmetric distance (row 1)
+ *                 after get_overlapping_sums (PESQ.py:227-228); NaN for rows under 20 frames
+ *          frames NULL or [batch, 2, Fcap] float32 (Fcap = fsem_pesq_frames(length)): per-frame
+ *                 symmetric / asymmetric disturbances after the frame weighting and the clamp at
+ *                 45 (PESQ.py:222-224); row b fills its first fsem_pesq_frames(lengths[b]) frames
+ */
+size_t fsem_pesq_distances_workspace_bytes(int64_t batch, int64_t length);
+int fsem_pesq_distances_f32(const float *bark, const float *power, int64_t batch, int64_t length,
+                            const int32_t *lengths, float *dist, float *frames, void *ws,
+                            size_t ws_bytes, void *stream);
 
 /* ---------------------------------------------------------------- STOI / ESTOI
  * Whole-metric entry: replaces STOI.compute_stoi + compute_metric

@@ -19,9 +19,24 @@ def pytest_configure(config):
 def load_golden(name: str):
     d = np.load(os.path.join(GOLDEN, f"{name}.npz"), allow_pickle=False)
     out = {k: d[k] for k in d.files}
+    if "clean_f32" in out:  # float32 rows stored as such (inputs off the int16 grid)
+        out["clean_f"], out["noisy_f"] = out["clean_f32"], out["noisy_f32"]
+        return out
     out["clean_f"] = out["clean"].astype(np.float32) / 32768.0
     out["noisy_f"] = out["noisy"].astype(np.float32) / 32768.0
     return out
+
+
+def edge_inputs(g, name: str):
+    """(clean, noisy) float32 tensors of edge case `name` of the edges_16k golden, rebuilt exactly as
+    tests/golden/make_golden.py fed them to the reference: codes / 32768 * scale + offset."""
+    import torch
+    k = list(g["names"]).index(name)
+    sc, oc, on = (float(v) for v in g["params"][k])
+    c = torch.from_numpy(g["clean"]).to(torch.float32) / 32768.0
+    n = torch.from_numpy(g["noisy"]).to(torch.float32) / 32768.0
+    scale = torch.tensor(sc, dtype=torch.float32)
+    return c * scale + torch.tensor(oc, dtype=torch.float32), n * scale + torch.tensor(on, dtype=torch.float32)
 
 
 PESQ_CASES = ["pesq_3s", "pesq_ragged", "pesq_10s", "pesq_hi_snr", "pesq_lo_snr", "pesq_wide"]

@@ -51,9 +51,17 @@ def pesq_case(name: str, batch: int, length: int, seed: int, snr=(-5.0, 25.0)):
         out["level_scale"] = ((aligned.double() * speech.double()).sum(1) / speech.double().square().sum(1)).numpy()
         bark = m.get_bark_bands(speech.clone())
         out["bark"] = bark.numpy().astype(np.float32)
+        # the per-frame disturbances are what get_disturbances hands to get_overlapping_sums
+        # (symmetric first, then asymmetric): captured from the reference's own call
+        frames = []
+        pooled = m.get_overlapping_sums
+        m.get_overlapping_sums = lambda d: (frames.append(d.clone()), pooled(d))[1]
         sym, asym = m.get_disturbances(clean, noisy)
+        m.get_overlapping_sums = pooled
         out["sym"] = sym.numpy()
         out["asym"] = asym.numpy()
+        out["sym_frames"] = frames[0].numpy().astype(np.float32)
+        out["asym_frames"] = frames[1].numpy().astype(np.float32)
     np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
     print(name, scores)
 
@@ -156,7 +164,105 @@ def tones_case(name: str, sr: int = 10000, length: int = 30000):
     print(name, out["stoi"], out["estoi"], out["stoi_seed1"] - out["stoi"], out["estoi_seed1"] - out["estoi"])
 
 
+def _reference_pesq(clean, noisy, fir: str = "") -> np.ndarray:
+    """The reference's PESQ(16000) scores with the shim's FIR evaluation order (FSEM_SHIM_FIR)."""
+    prev = os.environ.get("FSEM_SHIM_FIR")
+    os.environ["FSEM_SHIM_FIR"] = fir
+    try:
+        return np.array([d["PESQ"] for d in RefPESQ(16000, use_gpu=False)(clean, noisy)], dtype=np.float64)
+    finally:
+        if prev is None:
+            del os.environ["FSEM_SHIM_FIR"]
+        else:
+            os.environ["FSEM_SHIM_FIR"] = prev
+
+
+def _reference_stoi(clean, noisy, sr: int, seed: int):
+    import warnings
+    torch.manual_seed(seed)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        try:
+            res = RefSTOI(sample_rate=sr, use_gpu=False)(clean, noisy)
+        except TypeError:  # no segment anywhere (STOI.py:162-165, 205)
+            nan = np.full(clean.shape[0], np.nan)
+            return nan, nan
+    return np.array([r["STOI"] for r in res]), np.array([r["ESTOI"] for r in res])
+
+
+# Edge inputs (VERDICT r2 item 1): a speech-like int16-grid pair transformed in float32 by
+#   x = codes / 32768 * scale + offset
+# (torch float32 ops, so the GPU tests rebuild the exact inputs from the stored codes).  The
+# reference runs twice per metric: PESQ with the shim's two admissible FIR evaluation orders,
+# STOI/ESTOI with torch seeds 0 and 1 (its normalize() adds 1e-12 * randn, STOI.py:116) -- the
+# spread of the two runs is the reference's own order/seed sensitivity on that input.
+EDGES = {
+    "dc100_clean": (1.0, 100.0, 0.0),
+    "dc100_both": (1.0, 100.0, 100.0),
+    "dc1000_both": (1.0, 1000.0, 1000.0),
+    "scale_1e-15": (1e-15, 0.0, 0.0),
+    "scale_1e18": (1e18, 0.0, 0.0),
+}
+
+
+def edge_inputs(codes_c, codes_n, scale: float, off_c: float, off_n: float):
+    c = torch.as_tensor(codes_c).to(torch.float32) / 32768.0
+    n = torch.as_tensor(codes_n).to(torch.float32) / 32768.0
+    sc = torch.tensor(scale, dtype=torch.float32)
+    return c * sc + torch.tensor(off_c, dtype=torch.float32), n * sc + torch.tensor(off_n, dtype=torch.float32)
+
+
+def edge_case(name: str = "edges_16k"):
+    clean, noisy, _ = speech_like_pairs(3, 32000, 16000, seed=5, snr_low=0.0, snr_high=30.0)
+    codes_c, codes_n = to_int16(clean).numpy(), to_int16(noisy).numpy()
+    out = dict(clean=codes_c, noisy=codes_n, sample_rate=16000, names=np.array(list(EDGES)),
+               params=np.array(list(EDGES.values()), dtype=np.float64))
+    base_c, base_n = edge_inputs(codes_c, codes_n, 1.0, 0.0, 0.0)
+    out["base_pesq"] = _reference_pesq(base_c, base_n)
+    out["base_stoi"], out["base_estoi"] = _reference_stoi(base_c, base_n, 16000, 0)
+    for k, (sc, oc, on) in EDGES.items():
+        c, n = edge_inputs(codes_c, codes_n, sc, oc, on)
+        out[k + "_pesq"] = _reference_pesq(c, n)
+        out[k + "_pesq_f64fir"] = _reference_pesq(c, n, "f64")
+        out[k + "_stoi"], out[k + "_estoi"] = _reference_stoi(c, n, 16000, 0)
+        out[k + "_stoi_seed1"], out[k + "_estoi_seed1"] = _reference_stoi(c, n, 16000, 1)
+        print(k, out[k + "_pesq"], out[k + "_pesq_f64fir"], out[k + "_stoi"], out[k + "_stoi_seed1"],
+              out[k + "_estoi"], out[k + "_estoi_seed1"])
+    print("base", out["base_pesq"], out["base_stoi"], out["base_estoi"])
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
+
+
+def tone_probe_case(name: str = "tone_probe_10k"):
+    """tools/tone_probe.py's inputs at 10 kHz: full-scale float32 sinusoids (250 / 1000 / 3150 Hz)
+    against the tone + 1e-3 noise, and tone + 0.05 noise against the pure tone -- scores near 0
+    and 1 where the segment statistics correlate rounding-level fluctuations.  Stored as float32
+    rows (clean_f32 / noisy_f32); STOI(10000) with torch seeds 0 and 1."""
+    rng = np.random.default_rng(7)
+    L = 20000
+    t = np.arange(L) / 10000.0
+    c, d = [], []
+    for f in (250.0, 1000.0, 3150.0):
+        tone = np.sin(2 * np.pi * f * t).astype(np.float32)
+        c += [tone, tone + 0.05 * rng.standard_normal(L).astype(np.float32)]
+        d += [tone + 1e-3 * rng.standard_normal(L).astype(np.float32), tone]
+    c, d = np.stack(c).astype(np.float32), np.stack(d).astype(np.float32)
+    out = dict(clean_f32=c, noisy_f32=d, sample_rate=10000)
+    ct, dt = torch.from_numpy(c), torch.from_numpy(d)
+    out["stoi"], out["estoi"] = _reference_stoi(ct, dt, 10000, 0)
+    out["stoi_seed1"], out["estoi_seed1"] = _reference_stoi(ct, dt, 10000, 1)
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
+    print(name, out["stoi"], out["estoi"], out["stoi_seed1"] - out["stoi"], out["estoi_seed1"] - out["estoi"])
+
+
 CASES = {
+    "edges_16k": edge_case,
+    "tone_probe_10k": tone_probe_case,
+    "pesq_3s": lambda: pesq_case("pesq_3s", batch=4, length=48000, seed=1),
+    "pesq_ragged": lambda: pesq_case("pesq_ragged", batch=3, length=40077, seed=2),
+    "pesq_10s": lambda: pesq_case("pesq_10s", batch=2, length=160000, seed=3),
+    "pesq_hi_snr": lambda: pesq_case("pesq_hi_snr", batch=3, length=48000, seed=4, snr=(10.0, 10.0)),
+    "pesq_lo_snr": lambda: pesq_case("pesq_lo_snr", batch=3, length=48000, seed=4, snr=(-5.0, -5.0)),
+    "pesq_wide": lambda: pesq_case("pesq_wide", batch=6, length=32000, seed=8, snr=(10.0, 45.0)),
     "tones_10k": lambda: tones_case("tones_10k"),
     "rate_8k": lambda: rate_case("rate_8k", batch=3, length=24000, sr=8000, seed=11),
     "varlen_16k": lambda: varlen_case("varlen_16k", [48000, 33333, 20001, 40960, 5000, 27003], sr=16000, seed=12),
@@ -171,12 +277,7 @@ if __name__ == "__main__":
             CASES[name]()
         sys.exit(0)
     torch.set_num_threads(8)
-    pesq_case("pesq_3s", batch=4, length=48000, seed=1)
-    pesq_case("pesq_ragged", batch=3, length=40077, seed=2)      # L % 256 != 0 (PESQ.py:128 quirk)
-    pesq_case("pesq_10s", batch=2, length=160000, seed=3)
-    pesq_case("pesq_hi_snr", batch=3, length=48000, seed=4, snr=(10.0, 10.0))
-    pesq_case("pesq_lo_snr", batch=3, length=48000, seed=4, snr=(-5.0, -5.0))
-    pesq_case("pesq_wide", batch=6, length=32000, seed=8, snr=(10.0, 45.0))     # MOS 1.5..4.2
+    # pesq_ragged: L % 256 != 0 (PESQ.py:128 quirk); pesq_wide: MOS 1.5..4.2
     stoi_case("stoi_10k", batch=4, length=48000, sr=10000, seed=5)   # as tests/reference/test_stoi.py:10
     stoi_case("stoi_16k", batch=4, length=48000, sr=16000, seed=6)   # resampler exercised
     stoi_case("stoi_16k_10s", batch=2, length=160000, sr=16000, seed=7)

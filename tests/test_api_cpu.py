@@ -181,3 +181,16 @@ def test_reference_static_helpers():
     assert torch.allclose(x[[0, 2, 3]].mean(1), torch.zeros(3), atol=1e-6)
     assert torch.allclose(x[[0, 2, 3]].norm(dim=1), torch.ones(3), atol=1e-6)
     assert (x[1] == 0).all()
+
+
+def test_normalize_propagates_nonfinite():
+    """STOI.normalize: a NaN / Inf slice stays non-finite as in the reference (STOI.py:113-119);
+    only an exactly zero-variance slice maps to 0."""
+    from fast_speech_enhancement_metrics_amd import STOI
+    x = torch.randn(3, 30, generator=torch.Generator().manual_seed(1))
+    x[0, 5] = float("nan")
+    x[1, 7] = float("inf")
+    STOI.normalize(x, dim=1)
+    assert torch.isnan(x[0]).all()
+    assert not torch.isfinite(x[1]).all()
+    assert torch.isfinite(x[2]).all()

