@@ -5,18 +5,24 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-One step = PESQ-wb + STOI/ESTOI scores of this rank's batch (4096 pairs per GPU by default:
-BASELINE.json configs[1], 10 s @ 16 kHz fp32) through the fused joint entry
-``PESQ_STOI(16000, use_gpu=True).scores`` (fsem_pesq_stoi_f32: one read of the inputs, scores
-bitwise equal to the two separate API calls; ``--separate`` runs ``PESQ.scores`` +
-``STOI.scores`` instead), the RCCL all-gather of the per-utterance [B, 3] scores over xGMI
-(N > 1), and one device->host copy of the job's scores on rank 0.  The API's Python
-list-of-dict formatting is not included (see DESIGN.md for its cost).
+One step = the drop-in call ``PESQ_STOI(16000, use_gpu=True)(clean, noisy)`` on this rank's batch
+(4096 pairs per GPU by default: BASELINE.json configs[1], 10 s @ 16 kHz fp32) -> the list of
+{"PESQ", "STOI", "ESTOI"} dicts, timed as the reference times its metrics
+(benchmark_metrics.py:72-75: wall clock around ``metric(clean, noisy)``, list building included).
+The call runs the fused joint entry fsem_pesq_stoi_f32 (one read of the inputs; scores bitwise
+equal to the two separate API calls; ``--separate`` runs ``PESQ(...)`` + ``STOI(...)`` instead).
+With N > 1 ranks every rank also all-gathers the job's [B, 3] scores over RCCL (xGMI).
+``scores_path`` reports the engine API alone (``PESQ_STOI.scores`` + one device->host copy).
 Weak scaling: every rank owns its own shard of utterances, generated in HBM before timing.
 
+``--gpus N`` without a torch.distributed launcher starts the N ranks itself (a child
+``torch.distributed.run`` process, before this process touches the GPU); N above the visible
+device count is an error.
+
 Rank 0 prints ONE JSON line with the metric, the roofline of the dominant kernel
-(pesq_front<joint>: algorithmic bytes / its HIP-event-timed duration vs 8 TB/s) and the CPU
-baseline (the oracle CPU restatement on a bounded sample, single core).
+(pesq_front<joint>: algorithmic bytes / its HIP-event-timed duration vs 8 TB/s), the CPU
+baseline (the package's use_gpu=False path on the host's cores at batch 4 and 64, as
+SURVEY.md 8(d) / BASELINE.md ask) and the oracle CPU restatement beside it (``cpu_oracle``).
 """
 from __future__ import annotations
 
@@ -45,7 +51,8 @@ def parse():
                          "(workspace allocation, clocks)")
     ap.add_argument("--batch", type=int, default=4096, help="utterance pairs per GPU")
     ap.add_argument("--length", type=int, default=160000, help="samples per utterance (16 kHz)")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="oracle CPU leg time budget")
+    ap.add_argument("--cpu-calls", type=int, default=7, help="CPU-baseline calls per batch size")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=5)
     ap.add_argument("--separate", action="store_true", help="two API calls (PESQ, STOI) instead of the joint entry")
@@ -56,7 +63,7 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(clean, noisy, budget_s):
+def cpu_oracle(clean, noisy, budget_s):
     """Oracle CPU restatement (oracle/), one core, on a bounded sample of the same workload."""
     try:
         from threadpoolctl import threadpool_limits
@@ -90,32 +97,56 @@ def cpu_baseline(clean, noisy, budget_s):
                       f"oracle numpy/C restatement, {dt:.1f} s"}
 
 
-def cpu_mode(clean, noisy, calls=5, batch=4):
-    """Informational: the package's own use_gpu=False path -- the reference's CPU mode restated in
-    torch/scipy (_cpu.py) -- on `batch` pairs of the workload with torch's default thread pool,
-    median of `calls` calls; not the contract's cpu_baseline (the oracle)."""
+def host_cores():
+    """Threads of the host's share: OMP_NUM_THREADS where the launcher sets it (16 per GPU on the
+    MI355X boxes, whose os.cpu_count() is the whole machine), else every core."""
+    return max(1, int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1))
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(clean, noisy, batches=(4, 64), calls=7):
+    """The contract's CPU baseline: the package's use_gpu=False path -- the reference's CPU mode
+    restated in torch/scipy (_cpu.py) -- called as the drop-in ``PESQ_STOI(16000, use_gpu=False)
+    (clean, noisy)`` on `batches` pairs of the workload, on the host's cores
+    (``torch.set_num_threads``); per batch size the median of the calls left after dropping the
+    first int(0.15 n) + 1 (benchmark_metrics.py:82).  value = the largest batch's rate."""
     from fast_speech_enhancement_metrics_amd import PESQ_STOI
-    c, d = clean[:batch].cpu(), noisy[:batch].cpu()
     m = PESQ_STOI(16000, use_gpu=False)
     prev = torch.get_num_threads()
-    # the host's CPU share: OMP_NUM_THREADS where the launcher sets it (16 per GPU on the MI355X
-    # boxes), else every core
-    threads = max(1, int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1))
+    threads = host_cores()
     torch.set_num_threads(threads)
+    out = {}
     try:
-        m.scores(c, d)  # warm-up
-        ts = []
-        for _ in range(calls):
-            t0 = time.perf_counter()
-            m.scores(c, d)
-            ts.append(time.perf_counter() - t0)
+        for b in batches:
+            c, d = clean[:b].cpu(), noisy[:b].cpu()
+            ts = []
+            for _ in range(calls):
+                t0 = time.perf_counter()
+                m(c, d)
+                ts.append(time.perf_counter() - t0)
+            kept = sorted(ts[int(calls * 0.15) + 1:])
+            med = kept[len(kept) // 2]
+            out[b] = {"value": b / med, "ms_per_call": round(med * 1e3, 1), "calls": len(kept)}
     finally:
         torch.set_num_threads(prev)
-    ts.sort()
-    med = ts[len(ts) // 2]
-    return {"value": batch / med, "unit": "utterances/s", "cores": threads,
-            "sample": f"use_gpu=False path (torch/scipy), {batch} pairs x {clean.shape[1]} samples, "
-                      f"median of {calls} calls ({med * 1e3:.0f} ms)"}
+    big = max(batches)
+    return {"value": out[big]["value"], "unit": "utterances/s", "cores": threads, "kind": "port",
+            "sample": (f"use_gpu=False drop-in call PESQ_STOI(16000)(clean, noisy) -> list of dicts, "
+                       f"{clean.shape[1]} samples @16kHz, batch {big} (batch {min(batches)}: "
+                       f"{out[min(batches)]['value']:.1f} utt/s), median of {out[big]['calls']} calls after "
+                       f"dropping the first {calls - out[big]['calls']}; {threads} threads of {os.cpu_count()} "
+                       f"logical CPUs ({cpu_model()})"),
+            "batches": {str(b): v for b, v in out.items()}}
 
 
 def kernel_roofline(clean, noisy, reps, joint):
@@ -359,19 +390,40 @@ def run_c5(args, world, rank, dev, distributed):
                        "parallelism": f"dp{world} (LPT shards by 16 kHz-equivalent length)"}}), flush=True)
 
 
+def spawn_ranks(n: int) -> int:
+    """`--gpus N` without a launcher: start N ranks as a child torch.distributed.run process (this
+    process has not touched the GPU: device_count() does not initialise HIP on this image) and
+    return its exit code.  N above the visible devices is an error."""
+    import socket
+    import subprocess
+    visible = torch.cuda.device_count()
+    if n > visible:
+        print(f"bench.py: --gpus {n} but only {visible} HIP device(s) are visible", file=sys.stderr)
+        return 2
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     distributed = "WORLD_SIZE" in os.environ  # launched by torch.distributed.run (any N)
+    if distributed and world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started {world} ranks", file=sys.stderr)
     if distributed:
         # RCCL prints a version banner on the process's stdout at init: route native stdout to
         # stderr so the result line stays the only line on stdout
         out_fd = os.dup(1)
         os.dup2(2, 1)
         sys.stdout = os.fdopen(out_fd, "w", buffering=1)
-        import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
@@ -384,6 +436,7 @@ def main():
         return
 
     from fast_speech_enhancement_metrics_amd import PESQ, PESQ_STOI, STOI
+    from fast_speech_enhancement_metrics_amd.distributed import gather_scores
     from fast_speech_enhancement_metrics_amd.synthetic import speech_like_pairs
 
     B, L = args.batch, args.length
@@ -393,60 +446,55 @@ def main():
     stoi = STOI(16000, use_gpu=True)
     joint = PESQ_STOI(16000, use_gpu=True)
 
-    from fast_speech_enhancement_metrics_amd.distributed import gather_scores
-
     def step():
-        # per-rank engine work: PESQ-wb and STOI/ESTOI scores of this rank's 4096 pairs
+        # the drop-in call on this rank's pairs -> list of dicts (the reference's measured unit)
         if args.separate:
-            p = pesq.scores(clean, noisy)
-            s, e = stoi.scores(clean, noisy, 16000)
+            res = [{**a, **b} for a, b in zip(pesq(clean, noisy), stoi(clean, noisy))]
+        elif distributed:
+            res, local_scores = joint.call_with_scores(clean, noisy)
         else:
-            p, s, e = joint.scores(clean, noisy)
+            res = joint(clean, noisy)
+        if distributed:  # the job's scores on every rank: RCCL all-gather over xGMI
+            if args.separate:
+                local_scores = torch.tensor([[d["PESQ"], d["STOI"], d["ESTOI"]] for d in res], device=dev)
+            gather_scores(local_scores, world * B)
+        return res
+
+    def scores_step():
+        # engine API alone: scores on the device, one device->host copy
+        p, s, e = joint.scores(clean, noisy)
         local = torch.stack([p, s, e], dim=1)
-        full = gather_scores(local, world * B) if distributed else local  # RCCL all-gather (xGMI)
-        return full.cpu() if rank == 0 else None  # one device->host copy of the job's scores
+        full = gather_scores(local, world * B) if distributed else local
+        return full.cpu() if rank == 0 else None
 
     # the dominant kernel's roofline (HIP-event timed launches of its stage entry) first: the
     # GPU's clocks are still ramping during the first steps after the input generation
     roof = kernel_roofline(clean, noisy, args.kernel_reps, joint=not args.separate)
-    for _ in range(args.warmup):
-        step()
-
-    def barrier():
-        if distributed:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    barrier()
-    dt = time.perf_counter() - t0
-    if distributed:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    dt = _timed(step, args, dev, distributed)
     ms_per_step = dt / args.steps * 1e3
     value = world * B * args.steps / dt
+    dt_s = _timed(scores_step, args, dev, distributed)
 
-    out = None
     if rank == 0:
-        cpu = cpu_m = None
+        cpu = oracle = None
         if not args.no_cpu_baseline and world == 1:
-            cpu_m = cpu_mode(clean, noisy)
-            cpu = cpu_baseline(clean, noisy, args.cpu_seconds)
+            cpu = cpu_baseline(clean, noisy, batches=tuple(sorted({min(4, B), min(64, B)})), calls=args.cpu_calls)
+            oracle = cpu_oracle(clean, noisy, args.cpu_seconds)
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "utterances/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (speech-like harmonic source + AM noise, SNR U[-5,25] dB, int16 grid)",
-            "config": {"workload": ("PESQ-wb + STOI/ESTOI scores of 10 s @ 16 kHz fp32 pairs, "
-                                    + ("two API calls (PESQ.scores + STOI.scores)" if args.separate else
-                                       "fused joint entry PESQ_STOI.scores (one read of the inputs)")),
+            "config": {"workload": ("PESQ-wb + STOI/ESTOI of 10 s @ 16 kHz fp32 pairs through the drop-in call "
+                                    + ("PESQ(16000)(c, n) + STOI(16000)(c, n)" if args.separate else
+                                       "PESQ_STOI(16000, use_gpu=True)(c, n) (fused joint entry, one read of "
+                                       "the inputs)") + " -> list of dicts"),
                        "batch_per_gpu": B, "global_batch": world * B, "length": L, "sample_rate": 16000,
                        "parallelism": f"dp{world} (utterance shards, RCCL all-gather of scores)"},
-            "roofline": roof, "cpu_baseline": cpu, "cpu_mode": cpu_m,
+            "roofline": roof, "cpu_baseline": cpu, "cpu_oracle": oracle,
+            "scores_path": {"value": round(world * B * args.steps / dt_s, 2), "unit": "utterances/s",
+                            "ms_per_step": round(dt_s / args.steps * 1e3, 3),
+                            "what": "PESQ_STOI.scores + one device->host copy (no list of dicts)"},
         }
         print(json.dumps(out), flush=True)
     if distributed:

@@ -16,6 +16,18 @@ from .loudness import Loudness
 from .spectrogram import Spectrogram
 
 
+def _unit_rows(x: torch.Tensor, lengths=None) -> torch.Tensor:
+    """Rows scaled by a power of two (exact) to a peak in [1, 2) of their first lengths[b] samples;
+    zero / non-finite rows as they are."""
+    a = x.abs()
+    if lengths is not None:
+        t = torch.arange(x.shape[1], device=x.device)
+        a = torch.where(t[None, :] < torch.as_tensor(lengths, device=x.device).reshape(-1, 1), a, torch.zeros_like(a))
+    peak = a.amax(dim=1)
+    ex = torch.where((peak > 0) & torch.isfinite(peak), torch.floor(torch.log2(peak)), torch.zeros_like(peak))
+    return torch.ldexp(x, -ex[:, None].to(x.dtype))
+
+
 class PESQ(BaseMetric):
     higher_is_better = True
     EXPECTED_SAMPLING_RATE = 16000
@@ -87,10 +99,15 @@ class PESQ(BaseMetric):
     # remaining stages are short torch expressions on the metric's device.  Scores do not go
     # through these methods: compute_metric runs the whole engine in one call.
     def _front(self, speech: torch.Tensor):
-        """Engine front end on any number of rows -> (unscaled Bark bands [N, F, 49] float32,
-        sum of the squared band-pass output [N] float32)."""
+        """Engine front end on any number of rows -> (unscaled Bark bands [N, F, 49], sum of the
+        squared band-pass output [N]), float64.  Rows go in scaled by a power of two to a peak
+        in [1, 2) (exact) and the results come back at the rows' own scale in float64, so the
+        float32 stage outputs cannot overflow for any finite input."""
         x = as_rows(speech)
         N, L = x.shape
+        peak = x.abs().amax(dim=1)
+        ex = torch.where((peak > 0) & torch.isfinite(peak), torch.floor(torch.log2(peak)), torch.zeros_like(peak))
+        x = _unit_rows(x).contiguous()
         if L % 4 or N % 2:
             x = torch.nn.functional.pad(x, (0, (-L) % 4))
             if N % 2:
@@ -108,7 +125,8 @@ class PESQ(BaseMetric):
         _native.check(lib.fsem_pesq_front_f32(x[:h].data_ptr(), x[h:].data_ptr(), h, L, x.stride(0), None,
                                               bark.data_ptr(), power.data_ptr(), ws.data_ptr(), ws.numel(),
                                               _native.stream_handle(x.device)), "PESQ front")
-        return bark[:N, :, :F].transpose(1, 2), power[:N]
+        g = torch.exp2(2 * ex.double())
+        return bark[:N, :, :F].transpose(1, 2).double() * g[:, None, None], power[:N].double() * g
 
     def align_level(self, speech: torch.Tensor) -> torch.Tensor:
         """Rows scaled to band-pass power 1e7 (PESQ.py:92-102): x * sqrt(1e7 / P) with
@@ -116,7 +134,7 @@ class PESQ(BaseMetric):
         speech = torch.atleast_2d(speech)
         L = speech.shape[1]
         if speech.is_cuda:
-            p = self._front(speech)[1].double()
+            p = self._front(speech)[1]
         else:
             p = torch.from_numpy(_cpu.bandpass_power(speech.detach().to(torch.float64).numpy()))
         gain = _cpu.level_scale(p, L).sqrt().to(speech.device, speech.dtype)
@@ -139,7 +157,7 @@ class PESQ(BaseMetric):
         if not speech.is_cuda:
             return _cpu.bark_of_rows(speech).to(speech.device)
         bark, p = self._front(speech)
-        return bark.double() * _cpu.level_scale(p.double(), speech.shape[1])[:, None, None]
+        return bark * _cpu.level_scale(p, speech.shape[1])[:, None, None]
 
     def equalize_bark_bands(self, clean_bark_bands: torch.Tensor, noisy_bark_bands: torch.Tensor):
         """(clean, noisy) Bark bands after the band and frame power equalisation (PESQ.py:142-166)."""
@@ -166,8 +184,10 @@ class PESQ(BaseMetric):
         distance [B], per-frame disturbances [B, 2, F] -- symmetric then asymmetric, after the
         frame weighting and the clamp at 45, PESQ.py:222-224).  GPU only (the stage entry
         fsem_pesq_distances_f32); rows under 20 frames give NaN distances."""
-        clean = as_rows(clean_speech)
-        noisy = as_rows(noisy_speech)
+        # each signal is level-aligned on its own (PESQ.py:92-102), so scaling a row by a power of
+        # two changes nothing but the range: rows go in with peaks in [1, 2), as _front
+        clean = _unit_rows(as_rows(clean_speech), lengths)
+        noisy = _unit_rows(as_rows(noisy_speech), lengths)
         lib = _native.load()
         B, L = clean.shape
         F = lib.fsem_pesq_frames(L)

@@ -34,13 +34,14 @@ class STOI(BaseMetric):
 
     @staticmethod
     def normalize(x: torch.Tensor, dim: int = 0) -> torch.Tensor:
-        """In place, as STOI.py:113-119: centre along ``dim`` and divide by the L2 norm.  Without the
-        reference's ``1e-12 * randn`` term (deterministic, as the engine): a zero-variance slice
-        becomes 0 instead of a random unit vector.  Non-finite slices stay non-finite (NaN / Inf
+        """In place, as STOI.py:113-119: centre along ``dim`` and divide by the L2 norm, with the
+        reference's ``1e-12 * randn`` term taken in expectation (deterministic, as the engine):
+        the squared norm gains N * 1e-24 (N = x.shape[dim]) -- no change for any slice with a
+        spread above ~1e-8, 0 for a zero-variance slice (the reference: a random unit vector),
+        ~0 for a slice far below the noise.  Non-finite slices stay non-finite (NaN / Inf
         propagate as in the reference)."""
         x -= x.mean(dim=dim, keepdim=True)
-        n = torch.linalg.vector_norm(x, ord=2, dim=dim, keepdim=True)
-        x.copy_(torch.where(n == 0, torch.zeros_like(x), x / torch.where(n == 0, torch.ones_like(n), n)))
+        x /= torch.sqrt(x.square().sum(dim=dim, keepdim=True) + x.shape[dim] * 1e-24)
         return x
 
     # ------------------------------------------------------------------ reference attributes

@@ -5,7 +5,8 @@ Batched torch/scipy implementation of the same math the HIP engine runs:
   STOI: fast_se_metrics/STOI.py:26-205
 The level-alignment band-pass runs as a float64 second-order-section cascade and the
 pre-emphasis as a float64 IIR (scipy C loops); spectra via torch.stft.  STOI's
-``normalize`` is deterministic here (no 1e-12 * randn term; zero-variance rows map to 0).
+``normalize`` is deterministic here: its 1e-12 * randn term taken in expectation (zero-variance
+rows map to 0, rows far below 1e-12 to ~0, as the engine and the oracle).
 """
 from __future__ import annotations
 
@@ -177,9 +178,22 @@ _CLIP = 1 + 10 ** (15 / 20)
 
 
 def _norm(v: torch.Tensor, dim: int) -> torch.Tensor:
+    """STOI.py:113-119 in expectation over its 1e-12 * randn term: the squared norm gains
+    N * 1e-24 (N = the normalised dimension's size), the noise averages out of the products."""
     v = v - v.mean(dim=dim, keepdim=True)
-    n = v.norm(dim=dim, keepdim=True)
-    return torch.where(n > 0, v / torch.where(n > 0, n, torch.ones_like(n)), torch.zeros_like(v))
+    return v / torch.sqrt(v.square().sum(dim=dim, keepdim=True) + v.shape[dim] * 1e-24)
+
+
+def _estoi_norm(seg: torch.Tensor) -> torch.Tensor:
+    """Time, then band normalisation of [S, 15, 30] segments (STOI.py:178-181) in expectation over
+    both noise terms: the band normalisation's norm also takes the noise the time normalisation
+    left in each element (variance 1e-24 / its row's squared norm, x 14/15 after centring)."""
+    c = seg - seg.mean(dim=2, keepdim=True)
+    n2 = c.square().sum(dim=2, keepdim=True) + 30e-24
+    a = c / n2.sqrt()
+    a = a - a.mean(dim=1, keepdim=True)
+    q = a.square().sum(dim=1, keepdim=True) + (14 / 15) * (1e-24 / n2).sum(dim=1, keepdim=True) + 15e-24
+    return a / q.sqrt()
 
 
 def stoi(clean: torch.Tensor, noisy: torch.Tensor):
@@ -217,7 +231,7 @@ def stoi(clean: torch.Tensor, noisy: torch.Tensor):
         alpha = cx.norm(dim=2, keepdim=True) / (cy.norm(dim=2, keepdim=True) + 1e-9)
         yc = torch.minimum(cy * alpha, cx * _CLIP)
         out_s[b] = (_norm(cx, 2) * _norm(yc, 2)).sum() / 15 / nseg
-        out_e[b] = (_norm(_norm(cx, 2), 1) * _norm(_norm(cy, 2), 1)).sum() / 30 / nseg
+        out_e[b] = (_estoi_norm(cx) * _estoi_norm(cy)).sum() / 30 / nseg
     return out_s, out_e
 
 

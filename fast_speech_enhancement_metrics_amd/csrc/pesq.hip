@@ -18,7 +18,8 @@
 //        re-runs the five-section cascade from that state and sums y^2 over the samples its
 //        segment owns.  Filter state decays to <1e-11 within 16 chunks, so 4 levels suffice.
 //   C  taper of the first / last 15 samples (PESQ.py:108-109)
-//   D  pre-emphasis IIR (PESQ.py:111), same scan scheme (2 states), written back in place
+//   D  pre-emphasis IIR (PESQ.py:111), same scan scheme: FIR part first, then the all-pole
+//      part on states y[n-1], y[n-2] (as the reference's lfilter), written back in place
 //   E  Hann-512 frames, two frames per 512-point complex FFT (z = frame_a + i*frame_b,
 //      radix-8 Stockham, one wave per FFT, LDS exchange), |X|^2 split, DC zeroed; the
 //      spectra of the 48 frames are parked in the already-consumed part of the tile and the
@@ -130,6 +131,37 @@ __device__ __forceinline__ float taper_w(float tf, float Lf) {
   return __saturatef((tf + 1.f) * 0.0625f) * __saturatef((Lf - tf) * 0.0625f);
 }
 
+// Range of a tile: float32 squares and |X|^2 of the band-pass / pre-emphasis outputs stay
+// finite and normal for tile peaks within [2^-40, 2^40].  A tile whose peak lies outside is
+// scaled by 2^sh (its peak to [1, 2); exact in floating point) before the filters: the segment's
+// Bark bands and power partials then carry 2^(2 sh), recorded per (signal, segment) in pexp and
+// undone in the back end.  The reference divides both signals by their joint peak first
+// (equalize_ranges, PESQ.py:115-121), which cancels under the level alignment except for this
+// range: without the scaling, common scales of 1e-15 / 1e18 gave NaN / 4.64.
+__device__ __forceinline__ int range_shift(float peak) {
+  const uint32_t bits = __float_as_uint(peak);
+  const int ex = (int)((bits >> 23) & 0xff);  // biased exponent: 0 = zero / denormal, 255 = inf / NaN
+  if (ex == 0 || ex == 255 || (ex >= 127 - 40 && ex < 127 + 40)) return 0;
+  return 127 - ex;  // peak * 2^sh in [1, 2)
+}
+
+// Wave maximum of non-negative floats (as integers: same order), uniform result: DPP row
+// rotations, then row broadcasts (rows outside the mask read 0, the identity); lane 63 holds it.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_rot(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ float wave_max_pos(float v) {
+  uint32_t e = __float_as_uint(v);
+  e = max(e, dpp_rot<0x121>(e));  // row_ror:1
+  e = max(e, dpp_rot<0x122>(e));  // row_ror:2
+  e = max(e, dpp_rot<0x124>(e));  // row_ror:4
+  e = max(e, dpp_rot<0x128>(e));  // row_ror:8
+  e = max(e, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)e, 0x142, 0xA, 0xF, false));  // row_bcast:15
+  e = max(e, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)e, 0x143, 0xC, 0xF, false));  // row_bcast:31
+  return __uint_as_float(__builtin_amdgcn_readlane(e, 63));
+}
+
 struct Item {
   int64_t s;       // signal (0..B-1 ref, B..2B-1 deg)
   int g;           // segment
@@ -174,11 +206,24 @@ __device__ __forceinline__ void prefetch(const Item &it, int tid, float4 pre[PF]
   }
 }
 
+// Pre-emphasis FIR part (PESQ.py:111 via torchaudio's lfilter: FIR first, then the all-pole
+// part): w = b0 x[n] + b1 x[n-1] + b2 x[n-2] of the tapered input, h1 / h2 = x[n-1] / x[n-2].
+// The float32 numerator sums to exactly 0, so a DC offset cancels here and never enters the
+// all-pole states (kept as y[n-1], y[n-2]; gen_tables.py).
+__device__ __forceinline__ float pre_fir(float xp, float &h1, float &h2) {
+  const float w = fmaf(kPreB[0], xp, fmaf(kPreB[1], h1, kPreB[2] * h2));
+  h2 = h1;
+  h1 = xp;
+  return w;
+}
+
 // IIR pass 1: end states of this lane's chunk from zero state -- band-pass (states 0..9,
-// untapered input) and pre-emphasis (states 10..11, tapered input).  Fully unrolled: the
+// untapered input) and pre-emphasis all-pole part (states 10..11, driven by the FIR output of
+// the tapered input; h1 / h2: the two tapered samples before the chunk).  Fully unrolled: the
 // functionals (kScanG, __constant__) come in by scalar loads as SGPR operands.
 template <bool TAPER>
-__device__ __forceinline__ void iir_pass1(const float4 *__restrict__ my4, int64_t t_lane, int64_t L, float e[NS]) {
+__device__ __forceinline__ void iir_pass1(const float4 *__restrict__ my4, int64_t t_lane, int64_t L, float h1,
+                                          float h2, float e[NS]) {
   const float tf0 = (float)t_lane, Lf = (float)L;
   // opaque table pointer: the rows stay memory operands (s_load) instead of folded literals
   uint64_t gaddr = reinterpret_cast<uint64_t>(&kScanG[0][0]);
@@ -197,8 +242,9 @@ __device__ __forceinline__ void iir_pass1(const float4 *__restrict__ my4, int64_
 #pragma unroll
       for (int i = 0; i < NBP; ++i) e[i] = fmaf(G[n][i], xs[c], e[i]);
       const float xp = TAPER ? xs[c] * taper_w(tf0 + (float)n, Lf) : xs[c];
-      e[NBP] = fmaf(G[n][NBP], xp, e[NBP]);
-      e[NBP + 1] = fmaf(G[n][NBP + 1], xp, e[NBP + 1]);
+      const float w = pre_fir(xp, h1, h2);
+      e[NBP] = fmaf(G[n][NBP], w, e[NBP]);
+      e[NBP + 1] = fmaf(G[n][NBP + 1], w, e[NBP + 1]);
     }
   }
 }
@@ -213,10 +259,18 @@ __device__ __forceinline__ void iir_pass1(const float4 *__restrict__ my4, int64_
 constexpr int P_HI = (WARM + OWN) % CH, P_LO = WARM % CH;
 static_assert(P_HI % 4 == 0 && P_LO % 4 == 0 && P_HI < P_LO, "pass-2 power split points");
 
+// Pre-emphasis all-pole part of one sample: y = w - a1 y[n-1] - a2 y[n-2], states z[NBP] =
+// y[n-1], z[NBP + 1] = y[n-2].
+__device__ __forceinline__ float pre_ap(float w, float z[NS]) {
+  const float y = fmaf(-kPreA[1], z[NBP], fmaf(-kPreA[2], z[NBP + 1], w));
+  z[NBP + 1] = z[NBP];
+  z[NBP] = y;
+  return y;
+}
+
 template <bool TAPER, bool MASK>
 __device__ __forceinline__ void iir_pass2_group(float4 *__restrict__ w4, int q, float z[NS], float &acc, int own_lo,
-                                                int own_hi, int lim, float tf0, float Lf) {
-  const float b0 = kPreB[0], b1 = kPreB[1], b2 = kPreB[2], a1 = kPreA[1], a2 = kPreA[2];
+                                                int own_hi, int lim, float tf0, float Lf, float &h1, float &h2) {
   const float4 v = w4[q];
   float xs[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -232,9 +286,7 @@ __device__ __forceinline__ void iir_pass2_group(float4 *__restrict__ w4, int q, 
     }
     acc = (!MASK || (n >= own_lo && n < own_hi)) ? fmaf(u, u, acc) : acc;
     const float xp = TAPER ? xs[c] * taper_w(tf0 + (float)n, Lf) : xs[c];
-    const float y = fmaf(b0, xp, z[NBP]);
-    z[NBP] = fmaf(b1, xp, fmaf(-a1, y, z[NBP + 1]));
-    z[NBP + 1] = fmaf(b2, xp, -a2 * y);
+    const float y = pre_ap(pre_fir(xp, h1, h2), z);
     xs[c] = (!MASK || n < lim) ? y : 0.f;  // the reference zero-pads AFTER the filter (PESQ.py:128)
   }
   w4[q] = make_float4(xs[0], xs[1], xs[2], xs[3]);
@@ -242,11 +294,11 @@ __device__ __forceinline__ void iir_pass2_group(float4 *__restrict__ w4, int q, 
 
 template <bool TAPER>
 __device__ __forceinline__ float iir_pass2_masked(float4 *__restrict__ w4, float z[NS], int own_lo, int own_hi,
-                                                  int lim, int64_t t_lane, int64_t L) {
+                                                  int lim, int64_t t_lane, int64_t L, float h1, float h2) {
   const float tf0 = (float)t_lane, Lf = (float)L;
   float acc = 0.f;
 #pragma unroll 3
-  for (int q = 0; q < CH / 4; ++q) iir_pass2_group<TAPER, true>(w4, q, z, acc, own_lo, own_hi, lim, tf0, Lf);
+  for (int q = 0; q < CH / 4; ++q) iir_pass2_group<TAPER, true>(w4, q, z, acc, own_lo, own_hi, lim, tf0, Lf, h1, h2);
   return acc;
 }
 
@@ -273,22 +325,20 @@ __device__ __forceinline__ void bp_step(float x, float p[5], float z[NS], float 
 }
 
 // Pre-emphasis of one untapered sample (iir_pass2_group's second filter).
-__device__ __forceinline__ float pre_step(float xp, float z[NS]) {
-  const float y = fmaf(kPreB[0], xp, z[NBP]);
-  z[NBP] = fmaf(kPreB[1], xp, fmaf(-kPreA[1], y, z[NBP + 1]));
-  z[NBP + 1] = fmaf(kPreB[2], xp, -kPreA[2] * y);
-  return y;
+__device__ __forceinline__ float pre_step(float xp, float z[NS], float &h1, float &h2) {
+  return pre_ap(pre_fir(xp, h1, h2), z);
 }
 
 // Steady-state group q of the skewed pass: all five sections active; the power of group q-1
 // goes to acc.
-__device__ __forceinline__ void skew_group(float4 *__restrict__ w4, int q, float p[5], float z[NS], float &acc) {
+__device__ __forceinline__ void skew_group(float4 *__restrict__ w4, int q, float p[5], float z[NS], float &acc,
+                                           float &h1, float &h2) {
   const float4 v = w4[q];
   float xs[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     bp_step<0, 4>(xs[c], p, z, acc);
-    xs[c] = pre_step(xs[c], z);
+    xs[c] = pre_step(xs[c], z, h1, h2);
   }
   w4[q] = make_float4(xs[0], xs[1], xs[2], xs[3]);
 }
@@ -298,28 +348,29 @@ __device__ __forceinline__ void skew_group(float4 *__restrict__ w4, int q, float
 // of iir_pass2_group<false, false>, with four fill steps in group 0 and four drain steps after
 // group CH/4-1; the power of group r is summed while group r+1 is filtered.
 static_assert(P_HI >= 4, "group 0 lies in the first power part");
-__device__ __forceinline__ float iir_pass2_split(float4 *__restrict__ w4, float z[NS], int own_lo, int own_hi) {
+__device__ __forceinline__ float iir_pass2_split(float4 *__restrict__ w4, float z[NS], int own_lo, int own_hi,
+                                                float h1, float h2) {
   float a0 = 0.f, a1 = 0.f, a2 = 0.f;
   float p[5];
   {
     const float4 v = w4[0];
     float xs[4] = {v.x, v.y, v.z, v.w};
     bp_step<0, 0>(xs[0], p, z, a0);
-    xs[0] = pre_step(xs[0], z);
+    xs[0] = pre_step(xs[0], z, h1, h2);
     bp_step<0, 1>(xs[1], p, z, a0);
-    xs[1] = pre_step(xs[1], z);
+    xs[1] = pre_step(xs[1], z, h1, h2);
     bp_step<0, 2>(xs[2], p, z, a0);
-    xs[2] = pre_step(xs[2], z);
+    xs[2] = pre_step(xs[2], z, h1, h2);
     bp_step<0, 3>(xs[3], p, z, a0);
-    xs[3] = pre_step(xs[3], z);
+    xs[3] = pre_step(xs[3], z, h1, h2);
     w4[0] = make_float4(xs[0], xs[1], xs[2], xs[3]);
   }
 #pragma unroll
-  for (int q = 1; q < P_HI / 4 + 1; ++q) skew_group(w4, q, p, z, a0);
+  for (int q = 1; q < P_HI / 4 + 1; ++q) skew_group(w4, q, p, z, a0, h1, h2);
 #pragma unroll 3
-  for (int q = P_HI / 4 + 1; q < P_LO / 4 + 1; ++q) skew_group(w4, q, p, z, a1);
+  for (int q = P_HI / 4 + 1; q < P_LO / 4 + 1; ++q) skew_group(w4, q, p, z, a1, h1, h2);
 #pragma unroll
-  for (int q = P_LO / 4 + 1; q < CH / 4; ++q) skew_group(w4, q, p, z, a2);
+  for (int q = P_LO / 4 + 1; q < CH / 4; ++q) skew_group(w4, q, p, z, a2, h1, h2);
   bp_step<1, 4>(0.f, p, z, a2);
   bp_step<2, 4>(0.f, p, z, a2);
   bp_step<3, 4>(0.f, p, z, a2);
@@ -449,8 +500,8 @@ template <bool JOINT, bool VARLEN>
 __global__ void __launch_bounds__(PT, 2)
     pesq_front(const float *__restrict__ ref, const float *__restrict__ deg, int64_t B, int64_t Lcap,
                int64_t ld, const int32_t *__restrict__ lens_arg, int F, int npseg, int nseg, int64_t nitems,
-               float *__restrict__ bark, float *__restrict__ ppart, float *__restrict__ y10, int64_t y_ld,
-               float2 *__restrict__ vad, int64_t v_ld) {
+               float *__restrict__ bark, float *__restrict__ ppart, int *__restrict__ pexp,
+               float *__restrict__ y10, int64_t y_ld, float2 *__restrict__ vad, int64_t v_ld) {
   __shared__ __attribute__((aligned(16))) float tile[TILE + TILE_PAD];
   __shared__ __attribute__((aligned(16))) float xbuf[XBUF];
   __shared__ float red[8];
@@ -531,6 +582,7 @@ __global__ void __launch_bounds__(PT, 2)
     }
     if (VARLEN && it.g >= rg.nseg) {  // segment past this row's end: no samples, no frames
       if (tid < 4) ppart[(it.s * nseg + it.g) * 4 + tid] = 0.f;
+      if (tid == 0) pexp[it.s * nseg + it.g] = 0;
       const int64_t nxt = item + gridDim.x;
       if (nxt < nitems) prefetch(make_item(nxt, nseg, B, ld, Lcap, lens, ref, deg), tid, pre);
       continue;
@@ -538,8 +590,10 @@ __global__ void __launch_bounds__(PT, 2)
     STAMP(0);
     {
       float4 *t4 = reinterpret_cast<float4 *>(tile);
-      if (JOINT && it.tstart + TILE > L) {  // the row ends in this tile: the resampler sees zeros
-#pragma unroll                               // past it (torchaudio pads, base.py:20)
+      float pk = 0.f;  // peak |x| of the tile's row samples (range_shift)
+      auto peak4 = [](float m, float4 v) { return fmaxf(fmaxf(m, fmaxf(fabsf(v.x), fabsf(v.y))), fmaxf(fabsf(v.z), fabsf(v.w))); };
+      if (it.tstart + TILE > L) {  // the row ends in this tile: samples past it are not the row's
+#pragma unroll
         for (int k = 0; k < PF; ++k) {
           float4 v = pre[k];
           const int t = (int)(it.tstart - (L & ~(int64_t)3)) + 4 * (tid + PT * k);  // vs ceil4 start
@@ -550,12 +604,20 @@ __global__ void __launch_bounds__(PT, 2)
             v.z = (t == 0 && r > 2) ? v.z : 0.f;
             v.w = 0.f;
           }
-          t4[tid + PT * k] = v;
+          pk = peak4(pk, v);
+          // the joint resampler sees zeros past the row (torchaudio pads, base.py:20); the PESQ
+          // filters are causal and mask every output past L, so they may see the raw values
+          t4[tid + PT * k] = JOINT ? v : pre[k];
         }
       } else {
 #pragma unroll
-        for (int k = 0; k < PF; ++k) t4[tid + PT * k] = pre[k];
+        for (int k = 0; k < PF; ++k) {
+          pk = peak4(pk, pre[k]);
+          t4[tid + PT * k] = pre[k];
+        }
       }
+      pk = wave_max_pos(pk);
+      if (lane == 0) red[wave] = pk;
     }
     lds_barrier();
     STAMP(14);
@@ -569,6 +631,20 @@ __global__ void __launch_bounds__(PT, 2)
                     xbuf + RS_STAGE * wave, lane, wave);
     }
     STAMP(1);
+    // the tile's range shift (uniform): 0 for every tile whose peak lies in [2^-40, 2^40]
+    const int sh = __builtin_amdgcn_readfirstlane(range_shift(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
+    if (tid == 0) pexp[it.s * nseg + it.g] = sh;
+    if (sh != 0) {  // rare: a tile outside the safe range
+      if (JOINT) lds_barrier();  // the resampler's waves are done with the unscaled tile
+      float4 *c4 = reinterpret_cast<float4 *>(tile + CH * tid);
+#pragma unroll 1
+      for (int q = 0; q < CH / 4; ++q) {
+        const float4 v = c4[q];
+        c4[q] = make_float4(__builtin_amdgcn_ldexpf(v.x, sh), __builtin_amdgcn_ldexpf(v.y, sh),
+                            __builtin_amdgcn_ldexpf(v.z, sh), __builtin_amdgcn_ldexpf(v.w, sh));
+      }
+      lds_barrier();  // pass 1 reads the neighbouring chunk's last samples
+    }
     const int g = it.g;
     const int64_t tstart = it.tstart;
     const float4 *__restrict__ my4 = reinterpret_cast<const float4 *>(tile + CH * tid);
@@ -579,11 +655,22 @@ __global__ void __launch_bounds__(PT, 2)
 
     // ---------------------------------------------------------------- IIR pass 1: end states
     // band-pass (untapered input, PESQ.py:94) and pre-emphasis (tapered, PESQ.py:108-111)
+    // the two (tapered) samples before the chunk: the pre-emphasis FIR's history (zero at the
+    // tile start, as the zero state there); read before pass 2 rewrites the tile in place
+    float xm1 = 0.f, xm2 = 0.f;
+    if (tid > 0) {
+      xm1 = tile[CH * tid - 1];
+      xm2 = tile[CH * tid - 2];
+      if (__builtin_amdgcn_readfirstlane((int)wave_edge)) {
+        xm1 *= taper_w((float)(t_lane - 1), (float)L);
+        xm2 *= taper_w((float)(t_lane - 2), (float)L);
+      }
+    }
     float e[NS];
     if (__builtin_amdgcn_readfirstlane((int)wave_edge))
-      iir_pass1<true>(my4, t_lane, L, e);
+      iir_pass1<true>(my4, t_lane, L, xm1, xm2, e);
     else
-      iir_pass1<false>(my4, t_lane, L, e);
+      iir_pass1<false>(my4, t_lane, L, xm1, xm2, e);
     STAMP(2);
     // ---------------------------------------------------------------- chunk scan (4 levels)
     // double-buffered (read one buffer, write the other): one barrier per level.  Buffer A at
@@ -644,11 +731,11 @@ __global__ void __launch_bounds__(PT, 2)
       const bool split_ok = (own_lo <= 0 || own_lo == P_LO || own_lo >= CH) &&
                             (own_hi >= CH || own_hi == P_HI || own_hi <= 0) && lim >= CH;
       if (__builtin_amdgcn_readfirstlane((int)wave_edge))
-        acc = iir_pass2_masked<true>(w4, z, own_lo, own_hi, lim, t_lane, L);
+        acc = iir_pass2_masked<true>(w4, z, own_lo, own_hi, lim, t_lane, L, xm1, xm2);
       else if (__builtin_amdgcn_readfirstlane((int)__all(split_ok)))
-        acc = iir_pass2_split(w4, z, own_lo, own_hi);
+        acc = iir_pass2_split(w4, z, own_lo, own_hi, xm1, xm2);
       else
-        acc = iir_pass2_masked<false>(w4, z, own_lo, own_hi, lim, t_lane, L);
+        acc = iir_pass2_masked<false>(w4, z, own_lo, own_hi, lim, t_lane, L, xm1, xm2);
       // per-wave partials (no workgroup barrier); pesq_power_sum adds them in a fixed order
       const float tot = wave_sum(acc);
       if (lane == 0) ppart[(it.s * nseg + g) * 4 + wave] = tot * (kBpGain * kBpGain);
@@ -821,13 +908,29 @@ __global__ void __launch_bounds__(PT, 2)
   }
 }
 
-__global__ void __launch_bounds__(256) pesq_power_sum(const float *__restrict__ ppart, int nseg,
-                                                      int64_t nsig, float *__restrict__ power) {
+// Stage entry (fsem_pesq_front_f32): per-signal power sums of the partials, each segment's
+// range shift undone (an unrepresentable power becomes inf, as its true value would).
+__global__ void __launch_bounds__(256) pesq_power_sum(const float *__restrict__ ppart, const int *__restrict__ pexp,
+                                                      int nseg, int64_t nsig, float *__restrict__ power) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nsig) return;
   float acc = 0.f;
-  for (int g = 0; g < 4 * nseg; ++g) acc += ppart[s * nseg * 4 + g];
+  for (int g = 0; g < 4 * nseg; ++g) acc += __builtin_amdgcn_ldexpf(ppart[s * nseg * 4 + g], -2 * pexp[s * nseg + g / 4]);
   power[s] = acc;
+}
+
+// Stage entry: the Bark bands of range-shifted segments back to the input's scale (one thread
+// per (signal, band, frame); segments with shift 0 are left alone).
+__global__ void __launch_bounds__(256) pesq_bark_unshift(float *__restrict__ bark, const int *__restrict__ pexp,
+                                                         int nseg, int64_t nsig, int F) {
+  const int64_t fld = bark_ld(F);
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nsig * NBARK * fld) return;
+  const int f = (int)(i % fld);
+  const int64_t s = i / (NBARK * fld);
+  if (f >= F) return;
+  const int sh = pexp[s * nseg + f / NF];
+  if (sh != 0) bark[i] = __builtin_amdgcn_ldexpf(bark[i], -2 * sh);
 }
 
 // ------------------------------------------------------------------------------ back end
@@ -858,7 +961,7 @@ __device__ __forceinline__ float loud(float p, int b) {
 template <int BW, bool STAGE = false>
 __global__ void __launch_bounds__(64 * BW) __attribute__((amdgpu_waves_per_eu(4)))
     pesq_back(const float *__restrict__ bark, const float *__restrict__ power, const float *__restrict__ ppart,
-              int nseg, int64_t B, int64_t Lcap, const int32_t *__restrict__ lens, int Fcap,
+              const int *__restrict__ pexp, int nseg, int64_t B, int64_t Lcap, const int32_t *__restrict__ lens, int Fcap,
               float *__restrict__ scratch, float *__restrict__ mos, float *__restrict__ dist,
               float *__restrict__ frames) {
   constexpr int BT = 64 * BW;
@@ -898,18 +1001,37 @@ __global__ void __launch_bounds__(64 * BW) __attribute__((amdgpu_waves_per_eu(4)
   // PESQ.py:97-100 -- power = sum / (L + 5120) / 1.04684; bark scales by 1e7 / power
   // signal powers: given, or (ppart != nullptr, the whole-metric entries) summed here from the
   // front end's per-segment partials in pesq_power_sum's order -- one launch fewer per call
+  // With range-shifted segments (pesq_front's pexp), the partials are summed at the largest
+  // segment scale E (each scaled by 2^(-2 sh - E) <= 1) and frame f's bands by
+  // 2^(-2 sh(f) - E) on top of the level scale; with every shift 0 (every input whose tile
+  // peaks lie in [2^-40, 2^40]) the arithmetic is exactly the unshifted one.
   float pwc, pwn;
+  int eC = 0, eN = 0;             // E of clean / denoised
+  bool shc = false, shn = false;  // any segment shifted
   if (ppart) {
     __shared__ float pw_s[2];
+    __shared__ int pe_s[2], ps_s[2];
     if (tid < 2) {
       const float *__restrict__ q = ppart + (b + tid * B) * (int64_t)nseg * 4;
+      const int *__restrict__ ex = pexp + (b + tid * B) * (int64_t)nseg;
+      int emax = -(1 << 30), any = 0;
+      for (int g = 0; g < nseg; ++g) {
+        emax = max(emax, -2 * ex[g]);
+        any |= ex[g];
+      }
       float acc = 0.f;
-      for (int g = 0; g < 4 * nseg; ++g) acc += q[g];
+      for (int g = 0; g < 4 * nseg; ++g) acc += __builtin_amdgcn_ldexpf(q[g], -2 * ex[g >> 2] - emax);
       pw_s[tid] = acc;
+      pe_s[tid] = emax;
+      ps_s[tid] = any != 0;
     }
     lds_barrier();
     pwc = pw_s[0];
     pwn = pw_s[1];
+    eC = pe_s[0];
+    eN = pe_s[1];
+    shc = ps_s[0] != 0;
+    shn = ps_s[1] != 0;
   } else {
     pwc = power[b];
     pwn = power[b + B];
@@ -917,6 +1039,12 @@ __global__ void __launch_bounds__(64 * BW) __attribute__((amdgpu_waves_per_eu(4)
   const float pc = pwc / (float)(L + 5120) / 1.04684f;
   const float pn = pwn / (float)(L + 5120) / 1.04684f;
   const float sc = 1e7f / pc, sn = 1e7f / pn;
+  const int *__restrict__ exc = pexp ? pexp + b * (int64_t)nseg : nullptr;
+  const int *__restrict__ exn = pexp ? pexp + (b + B) * (int64_t)nseg : nullptr;
+  // the level scale of frame f (per lane: frames of one chunk may lie in two segments)
+  auto scale_at = [&](bool shifted, const int *__restrict__ ex, int E, float s0, int f) {
+    return shifted ? __builtin_amdgcn_ldexpf(s0, -2 * ex[f / NF] - E) : s0;
+  };
   const int nch = (F + 63) / 64;
 
   // ---- pass 1: silent frames (PESQ.py:146, loudness.py:48-53 x 1e2) and per-lane partial band
@@ -940,9 +1068,10 @@ __global__ void __launch_bounds__(64 * BW) __attribute__((amdgpu_waves_per_eu(4)
     asm volatile("" : "+s"(fs));  // per-chunk: keeps the 49 band offsets out of live SGPRs
     float aud[NBARK];  // audible clean power of each band (values, not compare masks: SGPRs)
     float a = 0.f;
+    const float scf = scale_at(shc, exc, eC, sc, fi);
 #pragma unroll
     for (int k = 0; k < NBARK; ++k) {
-      const float cl = ld(rcl, 4 * fi + k * fs, 0) * sc;
+      const float cl = ld(rcl, 4 * fi + k * fs, 0) * scf;
       aud[k] = (cl > kThresh[k] * 100.f) ? cl : 0.f;
       a += aud[k];
     }
@@ -985,9 +1114,10 @@ __global__ void __launch_bounds__(64 * BW) __attribute__((amdgpu_waves_per_eu(4)
     int fs = fstride;
     asm volatile("" : "+s"(fs));
     const bool keep = (BW == 1) ? ((keepm[c] >> lane) & 1ull) : ((f < F) && keepf[fi]);
+    const float snf = scale_at(shn, exn, eN, sn, fi);
 #pragma unroll
     for (int k = 0; k < NBARK; ++k) {
-      const float n = ld(rdn, 4 * fi + k * fs, 0) * sn;
+      const float n = ld(rdn, 4 * fi + k * fs, 0) * snf;
       acc[k] += (keep && n > kThresh[k] * 100.f) ? n : 0.f;
     }
   }
@@ -1022,10 +1152,11 @@ __global__ void __launch_bounds__(64 * BW) __attribute__((amdgpu_waves_per_eu(4)
     asm volatile("" : "+s"(fs));
     float ec[NBARK], ns[NBARK];
     float ac = 0.f, an = 0.f;
+    const float scf = scale_at(shc, exc, eC, sc, fi), snf = scale_at(shn, exn, eN, sn, fi);
 #pragma unroll
     for (int k = 0; k < NBARK; ++k) {
-      ec[k] = ratio_s[k] * (ld(rcl, 4 * fi + k * fs, 0) * sc);
-      ns[k] = ld(rdn, 4 * fi + k * fs, 0) * sn;
+      ec[k] = ratio_s[k] * (ld(rcl, 4 * fi + k * fs, 0) * scf);
+      ns[k] = ld(rdn, 4 * fi + k * fs, 0) * snf;
       ac += (ec[k] > kThresh[k]) ? ec[k] : 0.f;
       an += (ns[k] > kThresh[k]) ? ns[k] : 0.f;
     }
@@ -1127,9 +1258,15 @@ extern "C" int fsem_debug_read_stamps(void *dst, size_t bytes) {
 }
 #endif
 
+// front workspace: per-segment power partials [2B, nseg, 4] float, then the segments' range
+// shifts [2B, nseg] int (pesq_front's pexp)
+static size_t front_ppart_bytes(int64_t batch, int64_t length) {
+  return align_up(sizeof(float) * (size_t)(2 * batch) * (size_t)pesq::geometry(length).nseg * 4, 256);
+}
+
 extern "C" size_t fsem_pesq_front_workspace_bytes(int64_t batch, int64_t length) {
   const pesq::Geometry g = pesq::geometry(length);
-  return align_up(sizeof(float) * (size_t)(2 * batch) * (size_t)g.nseg * 4, 256);
+  return front_ppart_bytes(batch, length) + align_up(sizeof(int) * (size_t)(2 * batch) * (size_t)g.nseg, 256);
 }
 
 extern "C" size_t fsem_pesq_workspace_bytes(int64_t batch, int64_t length) {
@@ -1160,9 +1297,10 @@ int fsem::pesq::launch_front(const float *ref, const float *deg, int64_t batch, 
   }();
   const int64_t grid = std::min<int64_t>(nitems, (int64_t)ncu * wgs_per_cu);
   float *ppart = static_cast<float *>(ws);
+  int *pexp = reinterpret_cast<int *>(static_cast<char *>(ws) + front_ppart_bytes(batch, length));
 #define FSEM_FRONT(J, V)                                                                                \
   hipLaunchKernelGGL((pesq::pesq_front<J, V>), dim3((unsigned)grid), dim3(pesq::PT), 0, st, ref, deg, batch, \
-                     length, ld, lengths, g.F, g.npseg, g.nseg, nitems, bark, ppart, y10, y_ld, vad, v_ld)
+                     length, ld, lengths, g.F, g.npseg, g.nseg, nitems, bark, ppart, pexp, y10, y_ld, vad, v_ld)
   if (y10) {
     if (lengths) FSEM_FRONT(true, true);
     else FSEM_FRONT(true, false);
@@ -1173,8 +1311,13 @@ int fsem::pesq::launch_front(const float *ref, const float *deg, int64_t batch, 
 #undef FSEM_FRONT
   FSEM_CHECK_LAUNCH();
   if (!power_sums) return FSEM_OK;  // the back end sums the partials itself
+  // stage entry: the bands and powers at the input's own scale (include/fsem.h)
   hipLaunchKernelGGL(pesq::pesq_power_sum, dim3((unsigned)((2 * batch + 255) / 256)), dim3(256), 0, st,
-                     ppart, g.nseg, 2 * batch, power);
+                     ppart, pexp, g.nseg, 2 * batch, power);
+  FSEM_CHECK_LAUNCH();
+  const int64_t nb = 2 * batch * pesq::NBARK * pesq::bark_ld(g.F);
+  hipLaunchKernelGGL(pesq::pesq_bark_unshift, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, st, bark, pexp,
+                     g.nseg, 2 * batch, g.F);
   FSEM_CHECK_LAUNCH();
   return FSEM_OK;
 }
@@ -1235,9 +1378,13 @@ int fsem::pesq::launch_back(const float *bark, const float *power, const float *
   if (batch > 0x7fffffff) return FSEM_EINVAL;
   const int bw = pesq::back_waves(batch, length);
   float *scratch = static_cast<float *>(ws);
+  // with the front end's partials, its range shifts follow them (fsem_pesq_front_workspace_bytes)
+  const int *pexp = ppart ? reinterpret_cast<const int *>(reinterpret_cast<const char *>(ppart) +
+                                                          front_ppart_bytes(batch, length))
+                          : nullptr;
 #define FSEM_BACK(W, S, LDS)                                                                                   \
   hipLaunchKernelGGL((pesq::pesq_back<W, S>), dim3((unsigned)batch), dim3(64 * W), LDS, stream, bark, power, ppart, \
-                     g.nseg, batch, length, lengths, g.F, scratch, mos, dist, frames)
+                     pexp, g.nseg, batch, length, lengths, g.F, scratch, mos, dist, frames)
   if (dist || frames) {
     if (bw == 8) FSEM_BACK(8, true, 0);
     else if (bw == 4) FSEM_BACK(4, true, 0);

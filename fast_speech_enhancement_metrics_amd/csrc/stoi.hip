@@ -543,6 +543,7 @@ __global__ void __launch_bounds__(SEG_T, 3)
       // per-lane row statistics of the ESTOI time normalisation, kept in VGPRs: the band loop
       // stays rolled and writes them with its uniform index (register-indexed moves)
       f2 rxy[NB], nmr[NB];  // (1/|x - mu_x|, 1/|y - mu_y|), -(mu_x, mu_y) * rxy
+      f2 nvar = {0.f, 0.f};  // sum over bands of rxy^2: the time normalisation's noise variance / 1e-24
 #pragma unroll 1
       for (int j = 0; j < NB; ++j) {
         f2 v[NSEG];
@@ -577,15 +578,27 @@ __global__ void __launch_bounds__(SEG_T, 3)
           dcc = fmaf(dc, dc, dcc);
           dxc = fmaf(d.x, dc, dxc);
         }
-        // 1 / ||row - mean||; normalize() (STOI.py:113-119): a zero-variance row normalises to 0
-        const float rxn = dd.x > 0.f ? __builtin_amdgcn_rsqf(dd.x) : 0.f;
-        const float ryn = dd.y > 0.f ? __builtin_amdgcn_rsqf(dd.y) : 0.f;
-        const float rcn = dcc > 0.f ? __builtin_amdgcn_rsqf(dcc) : 0.f;
+        // normalize() (STOI.py:113-119) centres, adds 1e-12 * randn and divides by the norm: in
+        // expectation the squared norm gains N * 1e-24 (N = 30 frames) and the noise itself
+        // averages out of the correlation.  So 1 / sqrt(||row - mean||^2 + 30e-24): the same
+        // value for every row with ||row - mean||^2 > 5e-16 (the addend is below its rounding),
+        // 0 for a zero-variance row, ~0 for a row far below the noise (where the reference's
+        // own result is that noise: inputs at 1e-15 scale score ~0 +- 1e-2 there), and NaN / Inf
+        // rows propagate.
+        constexpr float kReg30 = 30e-24f;
+        const float rxn = __builtin_amdgcn_rsqf(dd.x + kReg30);
+        const float ryn = __builtin_amdgcn_rsqf(dd.y + kReg30);
+        const float rcn = __builtin_amdgcn_rsqf(dcc + kReg30);
         s_acc = fmaf(dxc * rxn, rcn, s_acc);
         rxy[j] = (f2){rxn, ryn};
+        nvar = __builtin_elementwise_fma(rxy[j], rxy[j], nvar);
         nmr[j] = -mu * rxy[j];
       }
-      // ESTOI: time-normalised rows, then band (column) normalisation (STOI.py:178-181)
+      // ESTOI: time-normalised rows, then band (column) normalisation (STOI.py:178-181).  The
+      // reference's time normalisation leaves noise of variance 1e-24 * rxy^2 in every element
+      // (negligible unless a row is near the 1e-12 noise itself), which the band normalisation's
+      // expected squared norm takes after centring (x 14/15), plus its own 15e-24.
+      const f2 breg = __builtin_elementwise_fma(nvar, (f2){14e-24f / 15.f, 14e-24f / 15.f}, (f2){15e-24f, 15e-24f});
       float e_acc = 0.f;
       for (int t = 0; t < NSEG; ++t) {
         f2 a[NB];
@@ -604,8 +617,8 @@ __global__ void __launch_bounds__(SEG_T, 3)
           q = __builtin_elementwise_fma(d, d, q);
           ac = fmaf(d.x, d.y, ac);
         }
-        const float ra = q.x > 0.f ? __builtin_amdgcn_rsqf(q.x) : 0.f;
-        const float rc = q.y > 0.f ? __builtin_amdgcn_rsqf(q.y) : 0.f;
+        const float ra = __builtin_amdgcn_rsqf(q.x + breg.x);
+        const float rc = __builtin_amdgcn_rsqf(q.y + breg.y);
         e_acc = fmaf(ac * ra, rc, e_acc);
       }
       st += (double)s_acc;

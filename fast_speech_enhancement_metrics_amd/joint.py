@@ -86,9 +86,27 @@ class PESQ_STOI(BaseMetric):
     def compute_metric(self, clean_speech: torch.Tensor | None, denoised_speech: torch.Tensor,
                        lengths=None) -> list[dict[str, float]]:
         assert clean_speech is not None
+        return self._listed(clean_speech, denoised_speech, lengths)[0]
+
+    def _listed(self, clean_speech, denoised_speech, lengths):
+        """(list of dicts, [B, 3] float32 scores on the metric's device) of 16 kHz rows."""
         with torch.inference_mode():
-            mos, s, e = (t.float() for t in self.scores(clean_speech, denoised_speech, lengths, sample_rate=16000))
-            m, s, e = torch.stack([mos, s, e]).tolist()
+            out = torch.stack([t.float() for t in self.scores(clean_speech, denoised_speech, lengths,
+                                                              sample_rate=16000)])
+            m, s, e = out.tolist()  # the one device -> host copy
         if all(x != x for x in s):  # as STOI (STOI.py:162-165)
-            warnings.warn("Not enough non-silent frames. Please check your sound files", RuntimeWarning, stacklevel=3)
-        return [{"PESQ": a, "STOI": b, "ESTOI": c} for a, b, c in zip(m, s, e)]
+            warnings.warn("Not enough non-silent frames. Please check your sound files", RuntimeWarning, stacklevel=4)
+        return [{"PESQ": a, "STOI": b, "ESTOI": c} for a, b, c in zip(m, s, e)], out.t()
+
+    def call_with_scores(self, clean_speech, denoised_speech, lengths=None):
+        """The drop-in call's list of dicts together with the same scores as a [B, 3] float32 tensor
+        (PESQ, STOI, ESTOI) on the metric's device -- for callers that also hand the scores on
+        (e.g. an all-gather across ranks) without rebuilding them from the dicts."""
+        if self.sample_rate != self.EXPECTED_SAMPLING_RATE:
+            res = self(clean_speech, denoised_speech, lengths)
+            t = torch.tensor([[d["PESQ"], d["STOI"], d["ESTOI"]] for d in res], dtype=torch.float32)
+            return res, t.to(self.device)
+        clean_speech, denoised_speech, lengths = self.split_ragged(clean_speech, denoised_speech, lengths)
+        clean_speech, denoised_speech = self.prepare_inputs(clean_speech, denoised_speech, lengths)
+        assert clean_speech is not None
+        return self._listed(clean_speech, denoised_speech, lengths)

@@ -6,8 +6,14 @@ Differences, all documented in DESIGN.md:
 
 * ``normalize`` (STOI.py:113-119) adds ``1e-12 * randn`` after centring -- a
   nondeterministic term that is below float32 resolution for non-degenerate rows.  The
-  oracle omits it and defines a zero-variance row as normalising to all-zeros (the
-  reference gives a random unit vector there).
+  oracle takes it in expectation: the noise averages out of the correlations and adds
+  N * 1e-24 to the expected squared norm (N = 30 frames, or 15 bands for ESTOI's second
+  normalisation), so a row normalises to (v - mean) / sqrt(||v - mean||^2 + N * 1e-24):
+  unchanged for any row above ~1e-8 in spread, 0 for a zero-variance row (the reference:
+  a random unit vector, contributing ~0 on average), ~0 for rows far below the noise
+  (inputs at 1e-15 scale: the reference scores that noise, ~0 +- 1e-2), NaN propagated.
+  ESTOI's band normalisation also takes the noise the time normalisation left in each element
+  (variance 1e-24 / (||v - mean||^2 + 30e-24), x 14/15 after centring) into its expected norm.
 * Per-utterance processing (the reference batches and zero-pads to the batch maximum;
   padded frames/segments are masked out by ``num_segments``, STOI.py:183-189, so the
   per-utterance result is the same).
@@ -105,11 +111,20 @@ def third_octave_bands(sig: np.ndarray) -> np.ndarray:
 
 
 def _normalize(v: np.ndarray, axis: int) -> np.ndarray:
+    """STOI.py:113-119 in expectation over its 1e-12 * randn term (module docstring)."""
     v = v - v.mean(axis=axis, keepdims=True)
-    nrm = np.sqrt((v ** 2).sum(axis=axis, keepdims=True))
-    with np.errstate(invalid="ignore", divide="ignore"):
-        out = np.where(nrm > 0, v / np.where(nrm > 0, nrm, 1.0), 0.0)
-    return out
+    return v / np.sqrt((v ** 2).sum(axis=axis, keepdims=True) + v.shape[axis] * 1e-24)
+
+
+def _estoi_normalize(seg: np.ndarray) -> np.ndarray:
+    """STOI.py:178-181 (time, then band normalisation) in expectation over both noise terms."""
+    c = seg - seg.mean(axis=2, keepdims=True)
+    n2 = (c ** 2).sum(axis=2, keepdims=True) + N_SEG * 1e-24
+    a = c / np.sqrt(n2)
+    a = a - a.mean(axis=1, keepdims=True)
+    q = (a ** 2).sum(axis=1, keepdims=True) + (NBANDS - 1) / NBANDS * (1e-24 / n2).sum(axis=1, keepdims=True) \
+        + NBANDS * 1e-24
+    return a / np.sqrt(q)
 
 
 def stoi_one(x: np.ndarray, y: np.ndarray, intermediates: dict | None = None):
@@ -140,8 +155,8 @@ def stoi_one(x: np.ndarray, y: np.ndarray, intermediates: dict | None = None):
     ds = _normalize(yeq, 2)
     stoi_sum = (cs * ds).sum() / NBANDS
     # ESTOI: time then band normalisation of the un-clipped segments
-    ce = _normalize(_normalize(xseg, 2), 1)
-    de = _normalize(_normalize(yseg, 2), 1)
+    ce = _estoi_normalize(xseg)
+    de = _estoi_normalize(yseg)
     estoi_sum = (ce * de).sum() / N_SEG
     if intermediates is not None:
         intermediates.update(stoi_seg=(cs * ds).sum(axis=(1, 2)) / NBANDS,

@@ -226,8 +226,12 @@ def edge_case(name: str = "edges_16k"):
         out[k + "_pesq_f64fir"] = _reference_pesq(c, n, "f64")
         out[k + "_stoi"], out[k + "_estoi"] = _reference_stoi(c, n, 16000, 0)
         out[k + "_stoi_seed1"], out[k + "_estoi_seed1"] = _reference_stoi(c, n, 16000, 1)
+        # STOI / ESTOI are scale-invariant (short of the 1e-9 / 1e-12 terms): the reference on
+        # 0.75 x the same pair is another float32 evaluation of the same scores
+        s75, e75 = _reference_stoi(c * 0.75, n * 0.75, 16000, 0)
+        out[k + "_stoi_x075"], out[k + "_estoi_x075"] = s75, e75
         print(k, out[k + "_pesq"], out[k + "_pesq_f64fir"], out[k + "_stoi"], out[k + "_stoi_seed1"],
-              out[k + "_estoi"], out[k + "_estoi_seed1"])
+              out[k + "_estoi"], out[k + "_estoi_seed1"], "x0.75:", s75 - out[k + "_stoi"], e75 - out[k + "_estoi"])
     print("base", out["base_pesq"], out["base_stoi"], out["base_estoi"])
     np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
 
@@ -250,8 +254,10 @@ def tone_probe_case(name: str = "tone_probe_10k"):
     ct, dt = torch.from_numpy(c), torch.from_numpy(d)
     out["stoi"], out["estoi"] = _reference_stoi(ct, dt, 10000, 0)
     out["stoi_seed1"], out["estoi_seed1"] = _reference_stoi(ct, dt, 10000, 1)
+    out["stoi_x075"], out["estoi_x075"] = _reference_stoi(ct * 0.75, dt * 0.75, 10000, 0)
     np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
-    print(name, out["stoi"], out["estoi"], out["stoi_seed1"] - out["stoi"], out["estoi_seed1"] - out["estoi"])
+    print(name, out["stoi"], out["estoi"], out["stoi_seed1"] - out["stoi"], out["estoi_seed1"] - out["estoi"],
+          out["stoi_x075"] - out["stoi"], out["estoi_x075"] - out["estoi"])
 
 
 CASES = {

@@ -25,10 +25,10 @@ def test_defaults_are_the_headline_config(monkeypatch):
     assert a.steps > 0 and a.warmup >= 0 and not a.separate
 
 
-def test_cpu_baseline_fields():
+def test_cpu_oracle_fields():
     from fast_speech_enhancement_metrics_amd.synthetic import speech_like_pairs
     c, n, _ = speech_like_pairs(2, 16000, 16000, seed=3)
-    out = bench.cpu_baseline(c, n, budget_s=0.0)  # one pair, then the budget stops it
+    out = bench.cpu_oracle(c, n, budget_s=0.0)  # one pair, then the budget stops it
     assert set(out) == {"value", "unit", "cores", "kind", "sample"}
     assert out["kind"] == "port" and out["cores"] == 1 and out["unit"] == "utterances/s"
     assert np.isfinite(out["value"]) and out["value"] > 0
@@ -46,8 +46,24 @@ def test_roofline_traffic_from_newest_pmc_summary():
     assert bench.pmc_traffic("pesq_front<true, false>", 64, 160000) == (None, None)  # other sizes: none
 
 
-def test_cpu_mode_fields():
+def test_cpu_baseline_is_the_use_gpu_false_path():
+    """cpu_baseline: the drop-in use_gpu=False call at two batch sizes on the host's cores, median
+    after dropping the first 15 % + 1 calls (benchmark_metrics.py:82)."""
     from fast_speech_enhancement_metrics_amd.synthetic import speech_like_pairs
-    c, n, _ = speech_like_pairs(2, 16000, 16000, seed=4)
-    out = bench.cpu_mode(c, n, calls=1, batch=2)
-    assert set(out) == {"value", "unit", "cores", "sample"} and out["value"] > 0
+    c, n, _ = speech_like_pairs(3, 16000, 16000, seed=4)
+    prev = torch.get_num_threads()
+    out = bench.cpu_baseline(c, n, batches=(1, 3), calls=3)
+    assert torch.get_num_threads() == prev
+    assert {"value", "unit", "cores", "kind", "sample", "batches"} <= set(out)
+    assert out["kind"] == "port" and out["cores"] == bench.host_cores() and out["value"] > 0
+    assert set(out["batches"]) == {"1", "3"} and out["batches"]["3"]["calls"] == 2
+    assert out["value"] == out["batches"]["3"]["value"]
+    assert "use_gpu=False" in out["sample"] and "threads" in out["sample"]
+
+
+def test_gpus_above_visible_devices_is_an_error(monkeypatch):
+    """--gpus N without a launcher spawns N ranks; more than the visible devices fails loudly."""
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2"])
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
+    assert bench.spawn_ranks(2) == 2

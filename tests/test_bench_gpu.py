@@ -14,7 +14,8 @@ REPO = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
 
 def test_bench_json_line_contract():
     out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--batch", "64", "--length", "48000",
-                          "--steps", "2", "--warmup", "1", "--kernel-reps", "2", "--cpu-seconds", "0.5"],
+                          "--steps", "2", "--warmup", "1", "--kernel-reps", "2", "--cpu-seconds", "0.5",
+                          "--cpu-calls", "2"],
                          cwd=REPO, capture_output=True, text=True, timeout=240)
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.strip()]
@@ -23,7 +24,7 @@ def test_bench_json_line_contract():
     with open(os.path.join(REPO, "BASELINE.json")) as f:
         assert d["metric"] == json.load(f)["metric"]
     for key in ("value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
-                "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline", "cpu_mode"):
+                "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline", "cpu_oracle", "scores_path"):
         assert key in d, key
     assert d["n_gpus"] == 1 and d["steps"] == 2 and d["warmup"] == 1 and d["higher_is_better"] is True
     assert d["value"] > 0 and abs(d["value"] - 64 * 1e3 / d["ms_per_step"]) < 1e-2 * d["value"]
@@ -33,5 +34,15 @@ def test_bench_json_line_contract():
     assert 0 < r["frac"] < 1 and abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
     assert r["traffic"] is None  # PMC traffic is only recorded at the bench configuration
     c = d["cpu_baseline"]
-    assert c["kind"] == "port" and c["cores"] == 1 and c["value"] > 0
-    assert d["cpu_mode"]["value"] > 0
+    assert c["kind"] == "port" and c["cores"] >= 1 and c["value"] > 0 and set(c["batches"]) == {"4", "64"}
+    assert d["cpu_oracle"]["cores"] == 1 and d["cpu_oracle"]["value"] > 0
+    assert d["scores_path"]["value"] > 0
+
+
+def test_bench_gpus_beyond_visible_fails():
+    """--gpus N without a launcher on a box with fewer devices: a clear error, not a 1-GPU run."""
+    import torch
+    n = torch.cuda.device_count() + 1
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(n), "--steps", "1"],
+                         cwd=REPO, capture_output=True, text=True, timeout=120)
+    assert out.returncode != 0 and "visible" in out.stderr and out.stdout.strip() == ""
