@@ -207,23 +207,28 @@ __device__ __forceinline__ void prefetch(const Item &it, int tid, float4 pre[PF]
 }
 
 // Pre-emphasis FIR part (PESQ.py:111 via torchaudio's lfilter: FIR first, then the all-pole
-// part): w = b0 x[n] + b1 x[n-1] + b2 x[n-2] of the tapered input, h1 / h2 = x[n-1] / x[n-2].
-// The float32 numerator sums to exactly 0, so a DC offset cancels here and never enters the
-// all-pole states (kept as y[n-1], y[n-2]; gen_tables.py).
-__device__ __forceinline__ float pre_fir(float xp, float &h1, float &h2) {
-  const float w = fmaf(kPreB[0], xp, fmaf(kPreB[1], h1, kPreB[2] * h2));
-  h2 = h1;
+// part).  The float32 numerator is exactly b0 (1, -2, 1) (b1 = -2 b0 and b2 = b0 in float32), so
+// w = b0 (x[n] - 2 x[n-1] + x[n-2]) = b0 ((x[n] - x[n-1]) - (x[n-1] - x[n-2])): the second
+// difference of the tapered input, formed from first differences (exact for neighbouring samples
+// within a factor 2 of each other), so a DC offset cancels exactly and never enters the all-pole
+// states.  b0 moves to the output (the FFT window carries it): the all-pole part runs on
+// yh = y / b0 driven by the second difference.  h1 = x[n-1], d1 = x[n-1] - x[n-2].
+__device__ __forceinline__ float pre_fir(float xp, float &h1, float &d1) {
+  const float d = xp - h1;
+  const float dd = d - d1;
+  d1 = d;
   h1 = xp;
-  return w;
+  return dd;
 }
 
 // IIR pass 1: end states of this lane's chunk from zero state -- band-pass (states 0..9,
-// untapered input) and pre-emphasis all-pole part (states 10..11, driven by the FIR output of
-// the tapered input; h1 / h2: the two tapered samples before the chunk).  Fully unrolled: the
-// functionals (kScanG, __constant__) come in by scalar loads as SGPR operands.
+// untapered input) and pre-emphasis all-pole part (states 10..11, driven by the second
+// difference of the tapered input; h1 / d1: pre_fir's history before the chunk).  Fully
+// unrolled: the functionals (kScanG, __constant__) come in by scalar loads as SGPR operands.
+// Returns the chunk's peak |x| (the taper zeroes samples past the row end in edge chunks).
 template <bool TAPER>
-__device__ __forceinline__ void iir_pass1(const float4 *__restrict__ my4, int64_t t_lane, int64_t L, float h1,
-                                          float h2, float e[NS]) {
+__device__ __forceinline__ float iir_pass1(const float4 *__restrict__ my4, int64_t t_lane, int64_t L, float h1,
+                                           float d1, float e[NS]) {
   const float tf0 = (float)t_lane, Lf = (float)L;
   // opaque table pointer: the rows stay memory operands (s_load) instead of folded literals
   uint64_t gaddr = reinterpret_cast<uint64_t>(&kScanG[0][0]);
@@ -232,6 +237,7 @@ __device__ __forceinline__ void iir_pass1(const float4 *__restrict__ my4, int64_
   crow *G = reinterpret_cast<crow *>(gaddr);
 #pragma unroll
   for (int i = 0; i < NS; ++i) e[i] = 0.f;
+  float pk = 0.f;
 #pragma unroll
   for (int q = 0; q < CH / 4; ++q) {
     const float4 v = my4[q];
@@ -242,11 +248,13 @@ __device__ __forceinline__ void iir_pass1(const float4 *__restrict__ my4, int64_
 #pragma unroll
       for (int i = 0; i < NBP; ++i) e[i] = fmaf(G[n][i], xs[c], e[i]);
       const float xp = TAPER ? xs[c] * taper_w(tf0 + (float)n, Lf) : xs[c];
-      const float w = pre_fir(xp, h1, h2);
+      pk = fmaxf(pk, fabsf(xp));
+      const float w = pre_fir(xp, h1, d1);
       e[NBP] = fmaf(G[n][NBP], w, e[NBP]);
       e[NBP + 1] = fmaf(G[n][NBP + 1], w, e[NBP + 1]);
     }
   }
+  return pk;
 }
 
 // IIR pass 2 from the true start state z: band-pass cascade (power over owned samples) and
@@ -514,7 +522,7 @@ __global__ void __launch_bounds__(PT, 2)
   float win[8];
   cf tw1[8], tw2[8];
 #pragma unroll
-  for (int r = 0; r < 8; ++r) win[r] = kHann512[lane + 64 * r];
+  for (int r = 0; r < 8; ++r) win[r] = kHann512[lane + 64 * r] * kPreB[0];  // x b0: pre_fir
   fft512_twiddles(lane, tw1, tw2);
   const int plane = (64 - lane) & 63;
   // Bark MFMA (v_mfma_f32_16x16x4_f32): wave w owns frame rows 16w..16w+15 of the segment and
@@ -590,10 +598,8 @@ __global__ void __launch_bounds__(PT, 2)
     STAMP(0);
     {
       float4 *t4 = reinterpret_cast<float4 *>(tile);
-      float pk = 0.f;  // peak |x| of the tile's row samples (range_shift)
-      auto peak4 = [](float m, float4 v) { return fmaxf(fmaxf(m, fmaxf(fabsf(v.x), fabsf(v.y))), fmaxf(fabsf(v.z), fabsf(v.w))); };
-      if (it.tstart + TILE > L) {  // the row ends in this tile: samples past it are not the row's
-#pragma unroll
+      if (JOINT && it.tstart + TILE > L) {  // the row ends in this tile: the resampler sees zeros
+#pragma unroll                               // past it (torchaudio pads, base.py:20)
         for (int k = 0; k < PF; ++k) {
           float4 v = pre[k];
           const int t = (int)(it.tstart - (L & ~(int64_t)3)) + 4 * (tid + PT * k);  // vs ceil4 start
@@ -604,20 +610,12 @@ __global__ void __launch_bounds__(PT, 2)
             v.z = (t == 0 && r > 2) ? v.z : 0.f;
             v.w = 0.f;
           }
-          pk = peak4(pk, v);
-          // the joint resampler sees zeros past the row (torchaudio pads, base.py:20); the PESQ
-          // filters are causal and mask every output past L, so they may see the raw values
-          t4[tid + PT * k] = JOINT ? v : pre[k];
+          t4[tid + PT * k] = v;
         }
       } else {
 #pragma unroll
-        for (int k = 0; k < PF; ++k) {
-          pk = peak4(pk, pre[k]);
-          t4[tid + PT * k] = pre[k];
-        }
+        for (int k = 0; k < PF; ++k) t4[tid + PT * k] = pre[k];
       }
-      pk = wave_max_pos(pk);
-      if (lane == 0) red[wave] = pk;
     }
     lds_barrier();
     STAMP(14);
@@ -631,20 +629,6 @@ __global__ void __launch_bounds__(PT, 2)
                     xbuf + RS_STAGE * wave, lane, wave);
     }
     STAMP(1);
-    // the tile's range shift (uniform): 0 for every tile whose peak lies in [2^-40, 2^40]
-    const int sh = __builtin_amdgcn_readfirstlane(range_shift(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
-    if (tid == 0) pexp[it.s * nseg + it.g] = sh;
-    if (sh != 0) {  // rare: a tile outside the safe range
-      if (JOINT) lds_barrier();  // the resampler's waves are done with the unscaled tile
-      float4 *c4 = reinterpret_cast<float4 *>(tile + CH * tid);
-#pragma unroll 1
-      for (int q = 0; q < CH / 4; ++q) {
-        const float4 v = c4[q];
-        c4[q] = make_float4(__builtin_amdgcn_ldexpf(v.x, sh), __builtin_amdgcn_ldexpf(v.y, sh),
-                            __builtin_amdgcn_ldexpf(v.z, sh), __builtin_amdgcn_ldexpf(v.w, sh));
-      }
-      lds_barrier();  // pass 1 reads the neighbouring chunk's last samples
-    }
     const int g = it.g;
     const int64_t tstart = it.tstart;
     const float4 *__restrict__ my4 = reinterpret_cast<const float4 *>(tile + CH * tid);
@@ -666,11 +650,17 @@ __global__ void __launch_bounds__(PT, 2)
         xm2 *= taper_w((float)(t_lane - 2), (float)L);
       }
     }
+    float h1 = xm1, d1 = xm1 - xm2;  // pre_fir's history at the chunk start
     float e[NS];
+    float pk;
     if (__builtin_amdgcn_readfirstlane((int)wave_edge))
-      iir_pass1<true>(my4, t_lane, L, xm1, xm2, e);
+      pk = iir_pass1<true>(my4, t_lane, L, h1, d1, e);
     else
-      iir_pass1<false>(my4, t_lane, L, xm1, xm2, e);
+      pk = iir_pass1<false>(my4, t_lane, L, h1, d1, e);
+    // the tile's peak |x| for its range shift (below): wave maxima, combined after the scan's
+    // first barrier
+    pk = wave_max_pos(pk);
+    if (lane == 0) red[wave] = pk;
     STAMP(2);
     // ---------------------------------------------------------------- chunk scan (4 levels)
     // double-buffered (read one buffer, write the other): one barrier per level.  Buffer A at
@@ -716,6 +706,29 @@ __global__ void __launch_bounds__(PT, 2)
       const float keep = (tid >= 1) ? 1.f : 0.f;
 #pragma unroll
       for (int i = 0; i < NS; ++i) z[i] = src[i] * keep;
+      // pre-emphasis: scan basis (u, v) -> direct-form states (y[n-1], y[n-2]) (gen_tables.py)
+      const float u = z[NBP], v = z[NBP + 1];
+      z[NBP] = fmaf(kPreToY[0][0], u, kPreToY[0][1] * v);
+      z[NBP + 1] = fmaf(kPreToY[1][0], u, kPreToY[1][1] * v);
+    }
+    // The tile's range shift (uniform, 0 for every tile whose peak lies in [2^-40, 2^40]).
+    // Pass 1 and the scan are linear and range-safe; squares (the band-pass power, |X|^2) come
+    // from pass 2 on, so a shifted tile scales its start states, the filters' history and its
+    // own chunk here -- exact powers of two, no barrier (pass 2 reads only the lane's chunk).
+    const int sh = __builtin_amdgcn_readfirstlane(range_shift(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
+    if (tid == 0) pexp[it.s * nseg + it.g] = sh;
+    if (sh != 0) {  // rare
+#pragma unroll
+      for (int i = 0; i < NS; ++i) z[i] = __builtin_amdgcn_ldexpf(z[i], sh);
+      xm1 = __builtin_amdgcn_ldexpf(xm1, sh);
+      xm2 = __builtin_amdgcn_ldexpf(xm2, sh);
+      float4 *c4 = reinterpret_cast<float4 *>(tile + CH * tid);
+#pragma unroll 1
+      for (int q = 0; q < CH / 4; ++q) {
+        const float4 v = c4[q];
+        c4[q] = make_float4(__builtin_amdgcn_ldexpf(v.x, sh), __builtin_amdgcn_ldexpf(v.y, sh),
+                            __builtin_amdgcn_ldexpf(v.z, sh), __builtin_amdgcn_ldexpf(v.w, sh));
+      }
     }
     STAMP(3);
 
@@ -731,11 +744,11 @@ __global__ void __launch_bounds__(PT, 2)
       const bool split_ok = (own_lo <= 0 || own_lo == P_LO || own_lo >= CH) &&
                             (own_hi >= CH || own_hi == P_HI || own_hi <= 0) && lim >= CH;
       if (__builtin_amdgcn_readfirstlane((int)wave_edge))
-        acc = iir_pass2_masked<true>(w4, z, own_lo, own_hi, lim, t_lane, L, xm1, xm2);
+        acc = iir_pass2_masked<true>(w4, z, own_lo, own_hi, lim, t_lane, L, xm1, xm1 - xm2);
       else if (__builtin_amdgcn_readfirstlane((int)__all(split_ok)))
-        acc = iir_pass2_split(w4, z, own_lo, own_hi, xm1, xm2);
+        acc = iir_pass2_split(w4, z, own_lo, own_hi, xm1, xm1 - xm2);
       else
-        acc = iir_pass2_masked<false>(w4, z, own_lo, own_hi, lim, t_lane, L, xm1, xm2);
+        acc = iir_pass2_masked<false>(w4, z, own_lo, own_hi, lim, t_lane, L, xm1, xm1 - xm2);
       // per-wave partials (no workgroup barrier); pesq_power_sum adds them in a fixed order
       const float tot = wave_sum(acc);
       if (lane == 0) ppart[(it.s * nseg + g) * 4 + wave] = tot * (kBpGain * kBpGain);

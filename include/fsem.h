@@ -25,6 +25,18 @@
  *    (instead of FSEM_ESHORT, which only the whole-batch form returns);
  *  - rows are at most 2^29 samples long (9.3 h at 16 kHz), before and after any resampling:
  *    the kernels address rows with 32-bit byte offsets; longer rows give FSEM_EINVAL;
+ *  - input domain (tests/test_edges_ref_gpu.py against the reference's own outputs,
+ *    tests/golden/edges_16k.npz, tone_probe_10k.npz):
+ *      PESQ: any finite scale (the PESQ front end shifts tiles whose peak lies outside
+ *        [2^-40, 2^40] by a power of two; measured at common scales 1e-15 and 1e18: within
+ *        1.2e-4 of the reference) and DC offsets (the pre-emphasis runs FIR first, as the
+ *        reference; +100 / +1000 on both signals: within 3e-3).
+ *      STOI/ESTOI: scale-invariant from about 1e-10 to 1e17; below, the reference's own
+ *        result is its 1e-12 * randn term (two seeds differ by 1e-2 around 0) and the engine
+ *        returns that term's expectation (~0); above, float32 |X|^2 overflows and both give
+ *        NaN.  Where the reference's float32 result itself moves by more than 1e-2 under an
+ *        exact re-scaling of the input (DC offsets ~1000x the signal, sinusoids whose
+ *        envelopes are flat to ~1e-6), the engine agrees to within twice that spread;
  *  - return 0 on success or a negative FSEM_E* code (fsem_strerror() for text);
  *  - re-entrant across streams / devices (launches use the current HIP device).
  */

@@ -57,3 +57,18 @@ def test_bench_config_rows_vs_oracle_and_batch_independence(batch):
     dp, ds, de = np.abs(mos[ROWS] - op).max(), np.abs(s[ROWS] - os_).max(), np.abs(e[ROWS] - oe).max()
     print(f"bench config rows {ROWS}: max |dPESQ| {dp:.2e} |dSTOI| {ds:.2e} |dESTOI| {de:.2e} vs oracle")
     assert dp < PESQ_TOL and ds < STOI_TOL and de < STOI_TOL
+
+
+def test_dropin_call_equals_scores_at_bench_size(batch):
+    """The drop-in call pipelines its host work over chunks (joint.py _listed): its dicts are the
+    one-call scores bitwise, in row order."""
+    from fast_speech_enhancement_metrics_amd import PESQ_STOI
+    c, n = batch
+    m = PESQ_STOI(16000, use_gpu=True)
+    assert c.shape[0] // m.pipeline_rows >= 2  # the pipelined form runs here
+    res = m(c, n)
+    mos, s, e = (t.cpu().numpy() for t in m.scores(c, n))
+    assert len(res) == B
+    np.testing.assert_array_equal(np.array([d["PESQ"] for d in res], dtype=np.float32), mos)
+    np.testing.assert_array_equal(np.array([d["STOI"] for d in res], dtype=np.float32), s)
+    np.testing.assert_array_equal(np.array([d["ESTOI"] for d in res], dtype=np.float32), e)

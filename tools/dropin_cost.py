@@ -38,7 +38,10 @@ def timeit(fn):
 
 out = {"batch": a.batch, "length": a.length}
 out["scores_plus_copy_ms"] = timeit(lambda: torch.stack(m.scores(c, n)).cpu())
-out["dropin_call_ms"] = timeit(lambda: m(c, n))
+for rows in (0, 2048, 1024):
+    m.pipeline_rows = rows
+    out[f"dropin_call_ms_pipeline_{rows}"] = timeit(lambda: m(c, n))
+m.pipeline_rows = 0
 host = torch.stack(m.scores(c, n)).cpu()
 t0 = time.perf_counter()
 for _ in range(a.reps):

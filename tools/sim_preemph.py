@@ -30,6 +30,25 @@ def tables(form):
     """(G [CH, 2], A[d] for d = 1, 2, 4, 8) of the 2-state pre-emphasis in the given basis."""
     if form == "allpoleH":
         form = "allpole"
+    if form == "normal":
+        # coupled (normal) form of the all-pole part: (u, v) = T (y[n-1], y[n-2]), u = y1 - r c y2,
+        # v = r s y2 -- ||M^k|| = r^k
+        r = np.sqrt(a[2])
+        c = -a[1] / (2 * r)
+        sn = np.sqrt(1 - c * c)
+        Tm = np.array([[1.0, -r * c], [0.0, r * sn]])
+        Gy, Ay = tables("allpole64")
+        return (Gy @ Tm.T).astype(f32), [(Tm @ A @ np.linalg.inv(Tm)).astype(f32) for A in Ay], Tm
+    if form == "allpole64":
+        M = np.array([[-a[1], -a[2]], [1.0, 0.0]])
+        K = np.array([1.0, 0.0])
+        G = np.zeros((CH, 2))
+        P = np.eye(2)
+        for k in range(CH - 1, -1, -1):
+            G[k] = P @ K
+            P = M @ P
+        Mch = np.linalg.matrix_power(M, CH)
+        return G, [np.linalg.matrix_power(Mch, d) for d in (1, 2, 4, 8)]
     if form == "df2t":
         M = np.array([[-a[1], 1.0], [-a[2], 0.0]])
         K = np.array([b[1] - a[1] * b[0], b[2] - a[2] * b[0]])
@@ -48,7 +67,8 @@ def tables(form):
 
 def tile_filter(x, form):
     """Pre-emphasis of one tile's samples x [TILE] (zero state at the tile start) -> y [TILE]."""
-    G, A = tables(form)
+    tb = tables(form)
+    G, A = tb[0], tb[1]
     ch = x.reshape(PT, CH).astype(f32)
     xm1 = np.concatenate([[0.0], ch[:-1, -1]]).astype(f32)  # x[-1], x[-2] of each chunk
     xm2 = np.concatenate([[0.0], ch[:-1, -2]]).astype(f32)
@@ -88,6 +108,10 @@ def tile_filter(x, form):
         e = new
     z = np.zeros_like(e)
     z[1:] = e[:-1]
+    if form == "normal":  # back to (y[n-1], y[n-2]) for the direct-form pass 2
+        Ti = np.linalg.inv(tb[2]).astype(f32)
+        z = np.stack([fma(Ti[0, 0], z[:, 0], (Ti[0, 1] * z[:, 1]).astype(f32)),
+                      fma(Ti[1, 0], z[:, 0], (Ti[1, 1] * z[:, 1]).astype(f32))], 1)
     y = np.empty_like(ch)
     if form == "df2t":
         z0, z1 = z[:, 0].copy(), z[:, 1].copy()
@@ -154,8 +178,14 @@ if __name__ == "__main__":
     for name in ("dc100_clean", "dc100_both", "dc1000_both"):
         c, n = (t.numpy() for t in edge_inputs(g, name))
         ref = g[name + "_pesq"]
-        for form in ("df2t", "allpole", "allpoleH"):
+        for form in ("df2t", "allpole", "normal"):
             print(f"{name:12s} {form:8s} sim - ref {np.round(pesq_with(c, n, form) - ref, 5)}")
     gb = load_golden("pesq_3s")
-    for form in ("df2t", "allpole"):
-        print(f"pesq_3s      {form:8s} sim - ref {np.round(pesq_with(gb['clean_f'], gb['noisy_f'], form) - gb['pesq'], 5)}")
+    x = gb["clean_f"].astype(f32)
+    exact = np.stack([po.ta.lfilter(np.ascontiguousarray(r[None]), po._PRE_A, po._PRE_B)[0] for r in x])
+    for form in ("df2t", "allpole", "normal"):
+        sim = np.stack([pre_emphasize_sim(np.concatenate([r[:15] / po._TAPER, r[15:-15], r[-15:] / po._TAPER[::-1]]), form)
+                        for r in x])
+        err = np.abs(sim.astype(np.float64) - exact).max() / np.abs(exact).max()
+        print(f"pesq_3s      {form:8s} sim - ref {np.round(pesq_with(gb['clean_f'], gb['noisy_f'], form) - gb['pesq'], 5)}"
+              f"  pre-emphasis max rel err vs sequential {err:.2e}")
