@@ -132,12 +132,19 @@ __device__ __forceinline__ float taper_w(float tf, float Lf) {
 }
 
 // Range of a tile: float32 squares and |X|^2 of the band-pass / pre-emphasis outputs stay
-// finite and normal for tile peaks within [2^-40, 2^40].  A tile whose peak lies outside is
-// scaled by 2^sh (its peak to [1, 2); exact in floating point) before the filters: the segment's
-// Bark bands and power partials then carry 2^(2 sh), recorded per (signal, segment) in pexp and
-// undone in the back end.  The reference divides both signals by their joint peak first
-// (equalize_ranges, PESQ.py:115-121), which cancels under the level alignment except for this
-// range: without the scaling, common scales of 1e-15 / 1e18 gave NaN / 4.64.
+// finite and normal for tile scales within [2^-40, 2^40] (the scale: the peak magnitude of the
+// chunks' pass-1 end states, which bound both filters' outputs to within their gains, a factor
+// ~100).  The main front-end pass only flags a signal with a tile outside that window (rare:
+// a worklist of signals in the workspace); the SAFE instance then redoes the flagged signals'
+// segments, each tile scaled by 2^sh (its scale to [1, 2); exact in floating point) from pass 2
+// on: the segment's Bark bands and power partials carry 2^(2 sh), recorded per (signal, segment)
+// in pexp and undone in the back end.  The reference divides both signals by their joint peak
+// first (equalize_ranges, PESQ.py:115-121), which cancels under the level alignment except for
+// this range: without the scaling, common scales of 1e-15 / 1e18 gave NaN / 4.64.
+__device__ __forceinline__ bool out_of_range(float peak) {
+  const int ex = (int)((__float_as_uint(peak) >> 23) & 0xff);
+  return peak != 0.f && (ex < 127 - 40 || ex >= 127 + 40);  // denormal / tiny, huge or Inf
+}
 __device__ __forceinline__ int range_shift(float peak) {
   const uint32_t bits = __float_as_uint(peak);
   const int ex = (int)((bits >> 23) & 0xff);  // biased exponent: 0 = zero / denormal, 255 = inf / NaN
@@ -223,12 +230,15 @@ __device__ __forceinline__ float pre_fir(float xp, float &h1, float &d1) {
 
 // IIR pass 1: end states of this lane's chunk from zero state -- band-pass (states 0..9,
 // untapered input) and pre-emphasis all-pole part (states 10..11, driven by the second
-// difference of the tapered input; h1 / d1: pre_fir's history before the chunk).  Fully
-// unrolled: the functionals (kScanG, __constant__) come in by scalar loads as SGPR operands.
-// Returns the chunk's peak |x| (the taper zeroes samples past the row end in edge chunks).
+// difference of the tapered input) -- as functionals of the chunk's first differences
+// (kScanG, gen_tables.py) plus the boundary terms of the samples before it: h1 = x[-1] and
+// d1 = x[-1] - x[-2] (tapered).  Fully unrolled: the functionals (__constant__) come in by
+// scalar loads as SGPR operands.  Edge chunks (TAPER) keep separate differences of the raw
+// (band-pass) and tapered (pre-emphasis) input; samples past the row end (up to ceil4(L): any
+// value) stay out of both, so out of the end states, which also decide the tile's range check.
 template <bool TAPER>
-__device__ __forceinline__ float iir_pass1(const float4 *__restrict__ my4, int64_t t_lane, int64_t L, float h1,
-                                           float d1, float e[NS]) {
+__device__ __forceinline__ void iir_pass1(const float4 *__restrict__ my4, int64_t t_lane, int64_t L, float h1,
+                                          float d1, float hr, float e[NS]) {
   const float tf0 = (float)t_lane, Lf = (float)L;
   // opaque table pointer: the rows stay memory operands (s_load) instead of folded literals
   uint64_t gaddr = reinterpret_cast<uint64_t>(&kScanG[0][0]);
@@ -236,8 +246,10 @@ __device__ __forceinline__ float iir_pass1(const float4 *__restrict__ my4, int64
   typedef const __attribute__((address_space(4))) float crow[NS];
   crow *G = reinterpret_cast<crow *>(gaddr);
 #pragma unroll
-  for (int i = 0; i < NS; ++i) e[i] = 0.f;
-  float pk = 0.f;
+  for (int i = 0; i < NBP; ++i) e[i] = kScanB[i] * hr;  // S x[-1] (untapered)
+  e[NBP] = kScanB[NBP] * d1;                            // -G2[0] d[-1] (tapered)
+  e[NBP + 1] = kScanB[NBP + 1] * d1;
+  float xr = hr;  // previous raw sample (TAPER: the band-pass's own history)
 #pragma unroll
   for (int q = 0; q < CH / 4; ++q) {
     const float4 v = my4[q];
@@ -245,16 +257,24 @@ __device__ __forceinline__ float iir_pass1(const float4 *__restrict__ my4, int64
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const int n = 4 * q + c;
+      float dp, db;
+      if (TAPER) {
+        const float xb = (t_lane + n >= L) ? 0.f : xs[c];
+        const float xp = xs[c] * taper_w(tf0 + (float)n, Lf);  // 0 past the row end
+        db = xb - xr;
+        xr = xb;
+        dp = xp - h1;
+        h1 = xp;
+      } else {
+        db = dp = xs[c] - h1;
+        h1 = xs[c];
+      }
 #pragma unroll
-      for (int i = 0; i < NBP; ++i) e[i] = fmaf(G[n][i], xs[c], e[i]);
-      const float xp = TAPER ? xs[c] * taper_w(tf0 + (float)n, Lf) : xs[c];
-      pk = fmaxf(pk, fabsf(xp));
-      const float w = pre_fir(xp, h1, d1);
-      e[NBP] = fmaf(G[n][NBP], w, e[NBP]);
-      e[NBP + 1] = fmaf(G[n][NBP + 1], w, e[NBP + 1]);
+      for (int i = 0; i < NBP; ++i) e[i] = fmaf(G[n][i], db, e[i]);
+      e[NBP] = fmaf(G[n][NBP], dp, e[NBP]);
+      e[NBP + 1] = fmaf(G[n][NBP + 1], dp, e[NBP + 1]);
     }
   }
-  return pk;
 }
 
 // IIR pass 2 from the true start state z: band-pass cascade (power over owned samples) and
@@ -504,12 +524,16 @@ __device__ __forceinline__ void resample_tile(const float *__restrict__ tile, in
 
 // Persistent: each workgroup walks items (signal, segment) = blockIdx.x, +gridDim.x, ...;
 // the next item's tile is in flight in registers while the current one is processed.
-template <bool JOINT, bool VARLEN>
+// rng: the range bookkeeping in the workspace -- pexp [2B * nseg] (per-segment shifts, zeroed
+// before the main pass), count [1], flags [2B] (zeroed), worklist [2B] of flagged signals.
+// SAFE (JOINT = false only): process the worklist's signals' segments with range shifts.
+template <bool JOINT, bool VARLEN, bool SAFE = false>
 __global__ void __launch_bounds__(PT, 2)
     pesq_front(const float *__restrict__ ref, const float *__restrict__ deg, int64_t B, int64_t Lcap,
                int64_t ld, const int32_t *__restrict__ lens_arg, int F, int npseg, int nseg, int64_t nitems,
-               float *__restrict__ bark, float *__restrict__ ppart, int *__restrict__ pexp,
+               float *__restrict__ bark, float *__restrict__ ppart, int *__restrict__ rng,
                float *__restrict__ y10, int64_t y_ld, float2 *__restrict__ vad, int64_t v_ld) {
+  static_assert(!(SAFE && JOINT), "the SAFE pass redoes PESQ only");
   __shared__ __attribute__((aligned(16))) float tile[TILE + TILE_PAD];
   __shared__ __attribute__((aligned(16))) float xbuf[XBUF];
   __shared__ float red[8];
@@ -573,12 +597,22 @@ __global__ void __launch_bounds__(PT, 2)
 #pragma unroll
   for (int ks = 0; ks < RS_KS; ++ks) rsb[ks] = JOINT ? kRsMfmaB.b[ks][lane] : 0.f;
 
+  int *__restrict__ const pexp = rng;
+  int *__restrict__ const rcount = rng + 2 * B * nseg;
+  int *__restrict__ const rflag = rcount + 1;
+  int *__restrict__ const rlist = rflag + 2 * B;
+  // SAFE: the worklist's items (signal rlist[i / nseg], segment i % nseg); usually none
+  const int64_t n_items = SAFE ? (int64_t)__builtin_amdgcn_readfirstlane(*rcount) * nseg : nitems;
+  auto item_at = [&](int64_t i) {
+    return SAFE ? (int64_t)rlist[i / nseg] * nseg + i % nseg : i;
+  };
   float4 pre[PF];
   int64_t item = blockIdx.x;
-  if (item < nitems) prefetch(make_item(item, nseg, B, ld, Lcap, lens, ref, deg), tid, pre);
+  if (!SAFE && item < n_items) prefetch(make_item(item_at(item), nseg, B, ld, Lcap, lens, ref, deg), tid, pre);
 
-  for (; item < nitems; item += gridDim.x) {
-    const Item it = make_item(item, nseg, B, ld, Lcap, lens, ref, deg);
+  for (; item < n_items; item += gridDim.x) {
+    const Item it = make_item(item_at(item), nseg, B, ld, Lcap, lens, ref, deg);
+    if (SAFE) prefetch(it, tid, pre);  // no pipelining in the rare pass
     const int64_t L = it.L;
     Geometry rg;  // this row's geometry (the launch's for uniform batches)
     if (VARLEN) {
@@ -590,9 +624,8 @@ __global__ void __launch_bounds__(PT, 2)
     }
     if (VARLEN && it.g >= rg.nseg) {  // segment past this row's end: no samples, no frames
       if (tid < 4) ppart[(it.s * nseg + it.g) * 4 + tid] = 0.f;
-      if (tid == 0) pexp[it.s * nseg + it.g] = 0;
       const int64_t nxt = item + gridDim.x;
-      if (nxt < nitems) prefetch(make_item(nxt, nseg, B, ld, Lcap, lens, ref, deg), tid, pre);
+      if (!SAFE && nxt < n_items) prefetch(make_item(item_at(nxt), nseg, B, ld, Lcap, lens, ref, deg), tid, pre);
       continue;
     }
     STAMP(0);
@@ -641,26 +674,37 @@ __global__ void __launch_bounds__(PT, 2)
     // band-pass (untapered input, PESQ.py:94) and pre-emphasis (tapered, PESQ.py:108-111)
     // the two (tapered) samples before the chunk: the pre-emphasis FIR's history (zero at the
     // tile start, as the zero state there); read before pass 2 rewrites the tile in place
-    float xm1 = 0.f, xm2 = 0.f;
+    float xm1 = 0.f, xm2 = 0.f, xr1 = 0.f;  // xr1: the raw x[-1] (the band-pass's history)
     if (tid > 0) {
-      xm1 = tile[CH * tid - 1];
+      xm1 = xr1 = tile[CH * tid - 1];
       xm2 = tile[CH * tid - 2];
       if (__builtin_amdgcn_readfirstlane((int)wave_edge)) {
+        xr1 = (t_lane - 1 >= L) ? 0.f : xr1;
         xm1 *= taper_w((float)(t_lane - 1), (float)L);
         xm2 *= taper_w((float)(t_lane - 2), (float)L);
       }
     }
-    float h1 = xm1, d1 = xm1 - xm2;  // pre_fir's history at the chunk start
     float e[NS];
-    float pk;
     if (__builtin_amdgcn_readfirstlane((int)wave_edge))
-      pk = iir_pass1<true>(my4, t_lane, L, h1, d1, e);
+      iir_pass1<true>(my4, t_lane, L, xm1, xm1 - xm2, xr1, e);
     else
-      pk = iir_pass1<false>(my4, t_lane, L, h1, d1, e);
-    // the tile's peak |x| for its range shift (below): wave maxima, combined after the scan's
-    // first barrier
-    pk = wave_max_pos(pk);
-    if (lane == 0) red[wave] = pk;
+      iir_pass1<false>(my4, t_lane, L, xm1, xm1 - xm2, xm1, e);
+    // The tile's scale for its range shift (below): the peak magnitude of the chunks' end
+    // states, which bound both filters' outputs -- the quantities squared from pass 2 on -- to
+    // within the filters' gains (a factor ~100, far inside the shift's [2^-40, 2^40] window);
+    // wave maxima, combined after the scan's first barrier.
+    {
+      float pk = 0.f;
+#pragma unroll
+      for (int i = 0; i < NS; ++i) pk = fmaxf(pk, fabsf(e[i]));
+      pk = wave_max_pos(pk);
+      if (SAFE) {
+        if (lane == 0) red[wave] = pk;  // combined after the scan's first barrier
+      } else if (lane == 0 && out_of_range(pk)) {
+        // rare: put the signal on the SAFE pass's worklist (once)
+        if (atomicExch(&rflag[it.s], 1) == 0) rlist[atomicAdd(rcount, 1)] = (int)it.s;
+      }
+    }
     STAMP(2);
     // ---------------------------------------------------------------- chunk scan (4 levels)
     // double-buffered (read one buffer, write the other): one barrier per level.  Buffer A at
@@ -715,9 +759,12 @@ __global__ void __launch_bounds__(PT, 2)
     // Pass 1 and the scan are linear and range-safe; squares (the band-pass power, |X|^2) come
     // from pass 2 on, so a shifted tile scales its start states, the filters' history and its
     // own chunk here -- exact powers of two, no barrier (pass 2 reads only the lane's chunk).
-    const int sh = __builtin_amdgcn_readfirstlane(range_shift(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
-    if (tid == 0) pexp[it.s * nseg + it.g] = sh;
-    if (sh != 0) {  // rare
+    int sh = 0;
+    if (SAFE) {
+      sh = __builtin_amdgcn_readfirstlane(range_shift(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
+      if (tid == 0) pexp[it.s * nseg + it.g] = sh;
+    }
+    if (SAFE && sh != 0) {
 #pragma unroll
       for (int i = 0; i < NS; ++i) z[i] = __builtin_amdgcn_ldexpf(z[i], sh);
       xm1 = __builtin_amdgcn_ldexpf(xm1, sh);
@@ -757,9 +804,9 @@ __global__ void __launch_bounds__(PT, 2)
     STAMP(4);
     // issue the next item's tile loads now: they stay in flight through the FFT / Bark
     // phases (the IIR phases above run without the prefetch registers live)
-    {
+    if (!SAFE) {
       const int64_t nxt = item + gridDim.x;
-      if (nxt < nitems) prefetch(make_item(nxt, nseg, B, ld, Lcap, lens, ref, deg), tid, pre);
+      if (nxt < n_items) prefetch(make_item(item_at(nxt), nseg, B, ld, Lcap, lens, ref, deg), tid, pre);
     }
 
     // ---------------------------------------------------------------- FFT rounds
@@ -932,18 +979,24 @@ __global__ void __launch_bounds__(256) pesq_power_sum(const float *__restrict__ 
   power[s] = acc;
 }
 
-// Stage entry: the Bark bands of range-shifted segments back to the input's scale (one thread
-// per (signal, band, frame); segments with shift 0 are left alone).
+// Stage entry: the Bark bands of range-shifted segments back to the input's scale: one thread
+// per (signal, segment), which returns at once unless that segment was shifted (the common case:
+// the launch costs a read of the shift array).
 __global__ void __launch_bounds__(256) pesq_bark_unshift(float *__restrict__ bark, const int *__restrict__ pexp,
                                                          int nseg, int64_t nsig, int F) {
-  const int64_t fld = bark_ld(F);
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nsig * NBARK * fld) return;
-  const int f = (int)(i % fld);
-  const int64_t s = i / (NBARK * fld);
-  if (f >= F) return;
-  const int sh = pexp[s * nseg + f / NF];
-  if (sh != 0) bark[i] = __builtin_amdgcn_ldexpf(bark[i], -2 * sh);
+  if (i >= nsig * nseg) return;
+  const int sh = pexp[i];
+  if (sh == 0) return;
+  const int64_t s = i / nseg;
+  const int g = (int)(i - s * nseg);
+  const int64_t fld = bark_ld(F);
+  const int f0 = g * NF, f1 = min(F, f0 + NF);
+  for (int k = 0; k < NBARK; ++k)
+    for (int f = f0; f < f1; ++f) {
+      float *p = bark + (s * NBARK + k) * fld + f;
+      *p = __builtin_amdgcn_ldexpf(*p, -2 * sh);
+    }
 }
 
 // ------------------------------------------------------------------------------ back end
@@ -1277,9 +1330,13 @@ static size_t front_ppart_bytes(int64_t batch, int64_t length) {
   return align_up(sizeof(float) * (size_t)(2 * batch) * (size_t)pesq::geometry(length).nseg * 4, 256);
 }
 
+// range bookkeeping after the partials: pexp [2B nseg], count, flags [2B], worklist [2B] (int)
+static size_t front_rng_ints(int64_t batch, int64_t length) {
+  return (size_t)(2 * batch) * (size_t)pesq::geometry(length).nseg + 1 + 4 * (size_t)batch;
+}
+
 extern "C" size_t fsem_pesq_front_workspace_bytes(int64_t batch, int64_t length) {
-  const pesq::Geometry g = pesq::geometry(length);
-  return front_ppart_bytes(batch, length) + align_up(sizeof(int) * (size_t)(2 * batch) * (size_t)g.nseg, 256);
+  return front_ppart_bytes(batch, length) + align_up(sizeof(int) * front_rng_ints(batch, length), 256);
 }
 
 extern "C" size_t fsem_pesq_workspace_bytes(int64_t batch, int64_t length) {
@@ -1310,17 +1367,25 @@ int fsem::pesq::launch_front(const float *ref, const float *deg, int64_t batch, 
   }();
   const int64_t grid = std::min<int64_t>(nitems, (int64_t)ncu * wgs_per_cu);
   float *ppart = static_cast<float *>(ws);
-  int *pexp = reinterpret_cast<int *>(static_cast<char *>(ws) + front_ppart_bytes(batch, length));
-#define FSEM_FRONT(J, V)                                                                                \
-  hipLaunchKernelGGL((pesq::pesq_front<J, V>), dim3((unsigned)grid), dim3(pesq::PT), 0, st, ref, deg, batch, \
-                     length, ld, lengths, g.F, g.npseg, g.nseg, nitems, bark, ppart, pexp, y10, y_ld, vad, v_ld)
+  int *rng = reinterpret_cast<int *>(static_cast<char *>(ws) + front_ppart_bytes(batch, length));
+  int *pexp = rng;
+  // shifts, worklist count and flags start at zero (the worklist itself is written before read)
+  if (hipMemsetAsync(rng, 0, sizeof(int) * ((size_t)(2 * batch) * g.nseg + 1 + 2 * (size_t)batch), st) != hipSuccess)
+    return FSEM_ELAUNCH;
+#define FSEM_FRONT(J, V, S)                                                                                      \
+  hipLaunchKernelGGL((pesq::pesq_front<J, V, S>), dim3((unsigned)grid), dim3(pesq::PT), 0, st, ref, deg, batch,  \
+                     length, ld, lengths, g.F, g.npseg, g.nseg, nitems, bark, ppart, rng, y10, y_ld, vad, v_ld)
   if (y10) {
-    if (lengths) FSEM_FRONT(true, true);
-    else FSEM_FRONT(true, false);
+    if (lengths) FSEM_FRONT(true, true, false);
+    else FSEM_FRONT(true, false, false);
   } else {
-    if (lengths) FSEM_FRONT(false, true);
-    else FSEM_FRONT(false, false);
+    if (lengths) FSEM_FRONT(false, true, false);
+    else FSEM_FRONT(false, false, false);
   }
+  FSEM_CHECK_LAUNCH();
+  // the range-safe pass over the flagged signals (an empty worklist: every workgroup exits at once)
+  if (lengths) FSEM_FRONT(false, true, true);
+  else FSEM_FRONT(false, false, true);
 #undef FSEM_FRONT
   FSEM_CHECK_LAUNCH();
   if (!power_sums) return FSEM_OK;  // the back end sums the partials itself
@@ -1328,7 +1393,7 @@ int fsem::pesq::launch_front(const float *ref, const float *deg, int64_t batch, 
   hipLaunchKernelGGL(pesq::pesq_power_sum, dim3((unsigned)((2 * batch + 255) / 256)), dim3(256), 0, st,
                      ppart, pexp, g.nseg, 2 * batch, power);
   FSEM_CHECK_LAUNCH();
-  const int64_t nb = 2 * batch * pesq::NBARK * pesq::bark_ld(g.F);
+  const int64_t nb = 2 * batch * g.nseg;
   hipLaunchKernelGGL(pesq::pesq_bark_unshift, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, st, bark, pexp,
                      g.nseg, 2 * batch, g.F);
   FSEM_CHECK_LAUNCH();

@@ -88,8 +88,12 @@ class PESQ_STOI(BaseMetric):
         assert clean_speech is not None
         return self._listed(clean_speech, denoised_speech, lengths)[0]
 
-    # Rows per chunk from which the drop-in call pipelines its host work (below); 0 disables.
-    pipeline_rows = 2048
+    # Rows per chunk from which the drop-in call pipelines its host work (below); 0 (default)
+    # disables it.  Measured at 4096 x 10 s (tools/dropin_cost.py, profiles/r3_a): one call 8.67 ms,
+    # 2 chunks 8.58 ms, 4 chunks 8.72 ms against 8.27 ms for the scores alone -- the host's list
+    # building (0.34 ms) mostly hides, but two half-size kernel sequences cost about as much GPU
+    # time as they hide, so it is off by default.
+    pipeline_rows = 0
 
     def _listed(self, clean_speech, denoised_speech, lengths):
         """(list of dicts, [B, 3] float32 scores on the metric's device) of 16 kHz rows.

@@ -101,3 +101,22 @@ def test_tone_probe_matches_reference():
         bar = max(0.01, 1.5 * _bar(ref, g[key + "_seed1"], g[key + "_x075"]))
         print("tone probe", key, "engine", got, "reference", ref, "x0.75", g[key + "_x075"], "bar", bar)
         np.testing.assert_allclose(got, ref, atol=bar, rtol=0)
+
+
+def test_padding_values_past_lengths_are_ignored():
+    """Per-row lengths with arbitrary padding (huge finite values, Inf, NaN) past each length:
+    the scores equal those of zero padding bitwise -- the padding neither enters a filter output
+    nor the PESQ tile range shift (include/fsem.h: values past `length` are never used)."""
+    from fast_speech_enhancement_metrics_amd import PESQ_STOI
+    g = load_golden("varlen_16k")
+    c = torch.from_numpy(g["clean_f"]).cuda()
+    n = torch.from_numpy(g["noisy_f"]).cuda()
+    lens = torch.from_numpy(g["lengths"]).cuda()
+    t = torch.arange(c.shape[1], device="cuda")[None, :]
+    past = t >= lens[:, None].long()
+    m = PESQ_STOI(16000, use_gpu=True)
+    ref = [x.cpu().numpy() for x in m.scores(c.masked_fill(past, 0.0), n.masked_fill(past, 0.0), lengths=lens)]
+    for fill in (1e30, -3e38, float("inf"), float("nan")):
+        got = [x.cpu().numpy() for x in m.scores(c.masked_fill(past, fill), n.masked_fill(past, fill), lengths=lens)]
+        for a, b in zip(got, ref):
+            np.testing.assert_array_equal(a, b)
