@@ -228,6 +228,19 @@ __device__ __forceinline__ float pre_fir(float xp, float &h1, float &d1) {
   return dd;
 }
 
+// Opaque first differences.  The IIR passes take the chunk's samples as first differences
+// x[n] - x[n-1]; the SLP vectoriser pairs two of them as (x[n], x[n+1]) - (x[n-1], x[n]) and
+// fetches the odd-aligned pair straight from LDS, splitting the chunk's float4 loads into b96 /
+// read2_b32 pieces (more LDS instructions, 4-way bank conflicts at the 52-float chunk stride).
+// An empty asm on the difference keeps it scalar: one v_sub per sample, ds_read_b128 loads.
+// (Applied on the hot paths -- pass 1 without taper, the split pass 2; in the masked pass 2 it
+// makes the compiler unroll the loop fully, +45 % VALU code.)
+__device__ __forceinline__ float opaque_diff(float a, float b) {
+  float d = a - b;
+  asm("" : "+v"(d));
+  return d;
+}
+
 // IIR pass 1: end states of this lane's chunk from zero state -- band-pass (states 0..9,
 // untapered input) and pre-emphasis all-pole part (states 10..11, driven by the second
 // difference of the tapered input) -- as functionals of the chunk's first differences
@@ -266,7 +279,7 @@ __device__ __forceinline__ void iir_pass1(const float4 *__restrict__ my4, int64_
         dp = xp - h1;
         h1 = xp;
       } else {
-        db = dp = xs[c] - h1;
+        db = dp = opaque_diff(xs[c], h1);
         h1 = xs[c];
       }
 #pragma unroll
@@ -294,6 +307,15 @@ __device__ __forceinline__ float pre_ap(float w, float z[NS]) {
   z[NBP + 1] = z[NBP];
   z[NBP] = y;
   return y;
+}
+
+// Pre-emphasis of one untapered sample, the split pass's (the same arithmetic as pre_fir + pre_ap).
+__device__ __forceinline__ float pre_step(float xp, float z[NS], float &h1, float &h2) {
+  const float d = opaque_diff(xp, h1);
+  const float dd = d - h2;
+  h2 = d;
+  h1 = xp;
+  return pre_ap(dd, z);
 }
 
 template <bool TAPER, bool MASK>
@@ -352,10 +374,6 @@ __device__ __forceinline__ void bp_step(float x, float p[5], float z[NS], float 
   }
 }
 
-// Pre-emphasis of one untapered sample (iir_pass2_group's second filter).
-__device__ __forceinline__ float pre_step(float xp, float z[NS], float &h1, float &h2) {
-  return pre_ap(pre_fir(xp, h1, h2), z);
-}
 
 // Steady-state group q of the skewed pass: all five sections active; the power of group q-1
 // goes to acc.
@@ -676,8 +694,14 @@ __global__ void __launch_bounds__(PT, 2)
     // tile start, as the zero state there); read before pass 2 rewrites the tile in place
     float xm1 = 0.f, xm2 = 0.f, xr1 = 0.f;  // xr1: the raw x[-1] (the band-pass's history)
     if (tid > 0) {
-      xm1 = xr1 = tile[CH * tid - 1];
-      xm2 = tile[CH * tid - 2];
+      // an opaque index: the load vectoriser would otherwise chain this 8-byte load with the
+      // chunk's float4 loads (passes 1 and 2) and split the chain at its 8-byte offset into
+      // b96 / read2 pieces (more LDS instructions, 4-way bank conflicts)
+      int hidx = CH * tid - 2;
+      asm volatile("" : "+v"(hidx));
+      const float2 hm = *reinterpret_cast<const float2 *>(tile + hidx);
+      xm1 = xr1 = hm.y;
+      xm2 = hm.x;
       if (__builtin_amdgcn_readfirstlane((int)wave_edge)) {
         xr1 = (t_lane - 1 >= L) ? 0.f : xr1;
         xm1 *= taper_w((float)(t_lane - 1), (float)L);
