@@ -190,7 +190,7 @@ def kernel_roofline(clean, noisy, reps, joint):
     ms = start.elapsed_time(end) / reps
     algo_bytes = 2 * B * L * 4  # both signals read once (2*L*4 B per pair)
     achieved = algo_bytes / (ms * 1e-3) / 1e9
-    name = "pesq_front<true, false>" if joint else "pesq_front<false, false>"
+    name = FRONT_KERNELS[joint]
     traffic, source = pmc_traffic(name, B, L)
     out = {"kernel": "pesq_front<joint>" if joint else "pesq_front", "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -208,8 +208,15 @@ def kernel_roofline(clean, noisy, reps, joint):
     return out
 
 
-def pmc_counter(kernel: str, counter: str, B: int, L: int):
-    """(value per launch, source) of one counter of `kernel` from the newest committed PMC summary."""
+# the uniform-length front-end instance in the PMC summaries' kernel names (joint / PESQ alone):
+# <JOINT, VARLEN, SAFE> from round 3 on, <JOINT, VARLEN> before
+FRONT_KERNELS = {True: ("pesq_front<true, false, false>", "pesq_front<true, false>"),
+                 False: ("pesq_front<false, false, false>", "pesq_front<false, false>")}
+
+
+def pmc_counter(kernel, counter: str, B: int, L: int):
+    """(value per launch, source) of one counter of `kernel` (a name suffix, or a tuple of them)
+    from the newest committed PMC summary."""
     import glob
     import re
     if (B, L) != (4096, 160000):
@@ -230,7 +237,7 @@ def pmc_counter(kernel: str, counter: str, B: int, L: int):
     return best
 
 
-def pmc_traffic(kernel: str, B: int, L: int):
+def pmc_traffic(kernel, B: int, L: int):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
     (profiles/*/pmc_summary.json, tools/pmc_summary.py: FETCH_SIZE x2 gfx950 correction +
     WRITE_SIZE, MI355X_MICROARCH.md 'HBM'), recorded at this same configuration; the counters

@@ -266,4 +266,4 @@ class PESQ(BaseMetric):
         assert clean_speech is not None
         with torch.inference_mode():
             mos = self.scores(clean_speech, denoised_speech, lengths, sample_rate=self.EXPECTED_SAMPLING_RATE)
-            return [{"PESQ": m} for m in mos.tolist()]
+            return _native.score_list(mos.reshape(1, -1).cpu(), ("PESQ",))

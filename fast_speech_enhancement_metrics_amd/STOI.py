@@ -194,11 +194,11 @@ class STOI(BaseMetric):
         return s, e
 
     def _finish(self, stois: torch.Tensor, estois: torch.Tensor) -> list[dict[str, float]]:
-        s, e = torch.stack([stois.float(), estois.float()]).tolist()
-        if all(x != x for x in s):  # no utterance has a 30-frame segment (STOI.py:162-165)
+        t = torch.stack([stois.float(), estois.float()]).cpu()
+        if bool(torch.isnan(t[0]).all()):  # no utterance has a 30-frame segment (STOI.py:162-165)
             warnings.warn("Not enough non-silent frames. Please check your sound files", RuntimeWarning, stacklevel=3)
             raise TypeError("iteration over a 0-d tensor")
-        return [{"STOI": a, "ESTOI": b} for a, b in zip(s, e)]
+        return _native.score_list(t, ("STOI", "ESTOI"))
 
     def _resample_cpu(self, x: torch.Tensor, sr: int) -> torch.Tensor:
         if sr == self.sample_rate:

@@ -11,6 +11,7 @@ import os
 import shutil
 import subprocess
 import sys
+import sysconfig
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG, "csrc")
@@ -20,6 +21,9 @@ STAMP_LIB = os.path.join(LIBDIR, "libfsem_stamps.so")  # diagnostic build (tools
 SOURCES = ["pesq.hip", "stoi.hip", "resample.hip"]
 HEADERS = ["fsem_common.h", "fsem_fft.h", "fsem_internal.h", "fsem_resample.h", "fsem_tables.inc"]
 ARCH = os.environ.get("FSEM_OFFLOAD_ARCH", "gfx950")
+# the drop-in call's list-of-dicts builder (host C, CPython API; csrc/score_list.c)
+SCORE_LIST_SRC = os.path.join(CSRC, "score_list.c")
+SCORE_LIST = os.path.join(LIBDIR, "_score_list" + sysconfig.get_config_var("EXT_SUFFIX"))
 
 
 def _hipcc() -> str:
@@ -55,7 +59,25 @@ def build(force: bool = False, verbose: bool = False, stamps: bool = False) -> s
     return lib
 
 
+def build_score_list(force: bool = False, verbose: bool = False) -> str:
+    """Compile the host-side list builder (gcc, no GPU) next to libfsem.so."""
+    if not force and os.path.exists(SCORE_LIST) and os.path.getmtime(SCORE_LIST) >= os.path.getmtime(SCORE_LIST_SRC):
+        return SCORE_LIST
+    os.makedirs(LIBDIR, exist_ok=True)
+    cc = os.environ.get("CC") or shutil.which("gcc") or shutil.which("cc")
+    if not cc:
+        raise RuntimeError("no C compiler found: the score-list builder cannot be built")
+    tmp = SCORE_LIST + f".{os.getpid()}.tmp"
+    cmd = [cc, "-O2", "-shared", "-fPIC", f"-I{sysconfig.get_paths()['include']}", "-o", tmp, SCORE_LIST_SRC]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd)
+    os.replace(tmp, SCORE_LIST)
+    return SCORE_LIST
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
+    print(build_score_list(force="--force" in sys.argv, verbose=True))
     if "--stamps" in sys.argv:
         print(build(verbose=True, stamps=True))

@@ -57,6 +57,34 @@ SIGNATURES = {
 }
 
 
+_score_list_mod = None
+
+
+def score_list(scores, keys: tuple) -> list:
+    """[{keys[k]: scores[k][b]} for b in range(B)] from a C-contiguous float32 [K, B] host array
+    (numpy, or a CPU tensor) -- the drop-in call's result list, built natively
+    (csrc/score_list.c; compiled by _build.build_score_list, built here on first use if absent)."""
+    global _score_list_mod
+    mod = _score_list_mod
+    if mod is None:
+        import importlib.machinery
+        import importlib.util
+
+        from . import _build
+        with _lock:
+            if _score_list_mod is None:
+                path = _build.build_score_list()
+                loader = importlib.machinery.ExtensionFileLoader("_score_list", path)
+                spec = importlib.util.spec_from_file_location("_score_list", path, loader=loader)
+                m = importlib.util.module_from_spec(spec)
+                loader.exec_module(m)
+                _score_list_mod = m
+        mod = _score_list_mod
+    if isinstance(scores, torch.Tensor):
+        scores = scores.detach().cpu().contiguous().numpy()
+    return mod.score_list(scores, keys)
+
+
 class NativeError(RuntimeError):
     pass
 

@@ -21,6 +21,9 @@ from .STOI import STOI
 from .base import BaseMetric, as_rows, check_row_rate, device_lengths
 
 
+_KEYS = ("PESQ", "STOI", "ESTOI")
+
+
 class PESQ_STOI(BaseMetric):
     higher_is_better = True
     EXPECTED_SAMPLING_RATE = 16000
@@ -88,12 +91,12 @@ class PESQ_STOI(BaseMetric):
         assert clean_speech is not None
         return self._listed(clean_speech, denoised_speech, lengths)[0]
 
-    # Rows per chunk from which the drop-in call pipelines its host work (below); 0 (default)
-    # disables it.  Measured at 4096 x 10 s (tools/dropin_cost.py, profiles/r3_a): one call 8.67 ms,
-    # 2 chunks 8.58 ms, 4 chunks 8.72 ms against 8.27 ms for the scores alone -- the host's list
-    # building (0.34 ms) mostly hides, but two half-size kernel sequences cost about as much GPU
-    # time as they hide, so it is off by default.
-    pipeline_rows = 0
+    # Rows per chunk from which the drop-in call pipelines its host work (below); 0 disables it.
+    # Measured at 4096 x 10 s (tools/dropin_cost.py): with the native list builder (0.21 ms per
+    # 4096 dicts) two chunks of 2048 take 8.29 ms per call against 8.39 ms for one (scores alone:
+    # 8.11 ms; profiles/r3_c/dropin.json); chunks of 1024 cost more GPU time than they hide
+    # (8.52 ms).  Batches under two chunks run as one call.
+    pipeline_rows = 2048
 
     def _listed(self, clean_speech, denoised_speech, lengths):
         """(list of dicts, [B, 3] float32 scores on the metric's device) of 16 kHz rows.
@@ -111,8 +114,7 @@ class PESQ_STOI(BaseMetric):
             if K <= 1:
                 out = torch.stack([t.float() for t in self.scores(clean_speech, denoised_speech, lengths,
                                                                   sample_rate=16000)])
-                m, s, e = out.tolist()  # the one device -> host copy
-                res = [{"PESQ": a, "STOI": b, "ESTOI": c} for a, b, c in zip(m, s, e)]
+                res = _native.score_list(out.cpu(), _KEYS)  # the one device -> host copy
             else:
                 clean = torch.atleast_2d(clean_speech)
                 lens = None if lengths is None else device_lengths(lengths, B, rows.shape[-1], rows.device)
@@ -133,10 +135,8 @@ class PESQ_STOI(BaseMetric):
                 res = []
                 for (lo, hi), ev in zip(bounds, done):
                     ev.synchronize()
-                    m, s, e = pinned[3 * lo:3 * hi].view(3, hi - lo).tolist()
-                    res.extend({"PESQ": a, "STOI": b, "ESTOI": c} for a, b, c in zip(m, s, e))
-                s = [d["STOI"] for d in res]
-        if all(x != x for x in s):  # as STOI (STOI.py:162-165)
+                    res.extend(_native.score_list(pinned[3 * lo:3 * hi].view(3, hi - lo).numpy(), _KEYS))
+        if all(d["STOI"] != d["STOI"] for d in res):  # as STOI (STOI.py:162-165)
             warnings.warn("Not enough non-silent frames. Please check your sound files", RuntimeWarning, stacklevel=4)
         return res, out.t()
 

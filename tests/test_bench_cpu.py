@@ -37,13 +37,13 @@ def test_cpu_oracle_fields():
 
 
 def test_roofline_traffic_from_newest_pmc_summary():
-    hbm, src = bench.pmc_traffic("pesq_front<true, false>", 4096, 160000)
+    hbm, src = bench.pmc_traffic(bench.FRONT_KERNELS[True], 4096, 160000)
     assert hbm is not None and hbm > 5_242_880_000  # at least the algorithmic input bytes
     rounds = sorted(os.listdir(os.path.join(REPO, "profiles")),
                     key=lambda p: [int(t) if t.isdigit() else t for t in __import__("re").split(r"(\d+)", p)])
     newest = [r for r in rounds if os.path.exists(os.path.join(REPO, "profiles", r, "pmc_summary.json"))][-1]
     assert src == os.path.join("profiles", newest, "pmc_summary.json")
-    assert bench.pmc_traffic("pesq_front<true, false>", 64, 160000) == (None, None)  # other sizes: none
+    assert bench.pmc_traffic(bench.FRONT_KERNELS[True], 64, 160000) == (None, None)  # other sizes: none
 
 
 def test_cpu_baseline_is_the_use_gpu_false_path():

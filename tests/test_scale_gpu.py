@@ -65,7 +65,7 @@ def test_dropin_call_equals_scores_at_bench_size(batch):
     from fast_speech_enhancement_metrics_amd import PESQ_STOI
     c, n = batch
     m = PESQ_STOI(16000, use_gpu=True)
-    m.pipeline_rows = 2048  # opt-in pipelined form
+    assert m.pipeline_rows == 2048  # the default: two chunks at the bench size
     res = m(c, n)
     m.pipeline_rows = 0
     assert [d["PESQ"] for d in res] == [d["PESQ"] for d in m(c, n)]

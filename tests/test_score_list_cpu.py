@@ -1,0 +1,48 @@
+"""The native list-of-dicts builder behind the drop-in calls (csrc/score_list.c): the same list
+the reference's BaseMetric.__call__ returns from tensor.tolist() (fast_se_metrics/base.py), for
+float32 and float64 scores, empty batches and NaN; malformed input raises."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from fast_speech_enhancement_metrics_amd import _native
+
+
+def _py(t, keys):
+    return [dict(zip(keys, r)) for r in zip(*t.tolist())]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+def test_matches_tolist(dtype):
+    g = torch.Generator().manual_seed(0)
+    t = torch.randn(3, 1000, generator=g, dtype=dtype)
+    t[1, 7] = float("nan")
+    t[0, 3] = float("inf")
+    keys = ("PESQ", "STOI", "ESTOI")
+    got = _native.score_list(t, keys)
+    ref = _py(t, keys)
+    assert len(got) == len(ref) == 1000
+    for a, b in zip(got, ref):
+        assert list(a) == list(keys)
+        for k in keys:
+            assert (math.isnan(a[k]) and math.isnan(b[k])) or a[k] == b[k]
+            assert type(a[k]) is float
+
+
+def test_single_key_and_empty():
+    assert _native.score_list(torch.tensor([[1.5, 2.0]]), ("PESQ",)) == [{"PESQ": 1.5}, {"PESQ": 2.0}]
+    assert _native.score_list(torch.empty(2, 0), ("STOI", "ESTOI")) == []
+    assert _native.score_list(np.zeros((2, 0), np.float32), ("STOI", "ESTOI")) == []
+
+
+def test_rejects_bad_input():
+    with pytest.raises(TypeError):
+        _native.score_list(np.zeros((3, 4), np.int32), ("a", "b", "c"))
+    with pytest.raises(TypeError):
+        _native.score_list(np.zeros(5, np.float32), ("a", "b", "c"))  # 5 values, 3 keys
+    with pytest.raises(ValueError):
+        _native.score_list(np.zeros((1, 4), np.float32), ())
+    with pytest.raises(TypeError):
+        _native.score_list(np.zeros((1, 4), np.float32), (1,))
