@@ -32,8 +32,16 @@ class PESQ(BaseMetric):
     higher_is_better = True
     EXPECTED_SAMPLING_RATE = 16000
 
-    def __init__(self, sample_rate: int = 16000, use_gpu: bool = False):
+    def __init__(self, sample_rate: int = 16000, use_gpu: bool = False, *, time_align: bool = False,
+                 max_delay: int = 16000):
+        """``time_align`` (extension, off by default as in the reference, PESQ.py:19-22): shift each
+        degraded row by its estimated delay before scoring (``alignment.time_align``, P.862-style;
+        ``max_delay`` samples at 16 kHz bounds the search).  The delays of the last scored batch
+        are kept in ``last_delays``."""
         super().__init__(sample_rate, use_gpu)
+        self.time_align = bool(time_align)
+        self.max_delay = int(max_delay)
+        self.last_delays = None
 
     @staticmethod
     def equalize_ranges(clean_speech: torch.Tensor, noisy_speech: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
@@ -238,6 +246,9 @@ class PESQ(BaseMetric):
         B, L = clean.shape
         if noisy.shape != clean.shape:
             raise Exception("`clean_speech` and `denoised_speech` should have the same shape.")
+        if getattr(self, "time_align", False):
+            from .alignment import time_align
+            noisy, self.last_delays = time_align(clean, noisy, lengths, self.max_delay)
         lib = _native.load() if clean.is_cuda else None
         if lib is None:
             if lengths is None:

@@ -18,7 +18,7 @@ CSRC = os.path.join(PKG, "csrc")
 LIBDIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIBDIR, "libfsem.so")
 STAMP_LIB = os.path.join(LIBDIR, "libfsem_stamps.so")  # diagnostic build (tools/stamps.py)
-SOURCES = ["pesq.hip", "stoi.hip", "resample.hip"]
+SOURCES = ["pesq.hip", "stoi.hip", "resample.hip", "align.hip"]
 HEADERS = ["fsem_common.h", "fsem_fft.h", "fsem_internal.h", "fsem_resample.h", "fsem_tables.inc"]
 ARCH = os.environ.get("FSEM_OFFLOAD_ARCH", "gfx950")
 # the drop-in call's list-of-dicts builder (host C, CPython API; csrc/score_list.c)

@@ -253,3 +253,79 @@ def per_row(fn, clean: torch.Tensor, noisy: torch.Tensor, lengths: torch.Tensor)
         return tuple(torch.cat([o[i] if o is not None else torch.full((1,), nan, dtype=torch.float64) for o in outs])
                      for i in range(len(proto)))
     return torch.cat([o if o is not None else torch.full((1,), nan, dtype=torch.float64) for o in outs])
+
+
+# ----------------------------------------------------------------------------- time alignment
+# The opt-in P.862-style delay estimation (not in the reference, PESQ.py:19-22; engine:
+# csrc/align.hip, which documents the stages), float64 with FFT cross-correlations.
+_TA_FRAME, _TA_FINE, _TA_ITERS = 64, 383, 12
+
+
+def _ta_envelope(x: np.ndarray) -> np.ndarray:
+    nfr = x.shape[0] // _TA_FRAME
+    e = np.square(x[:nfr * _TA_FRAME].reshape(nfr, _TA_FRAME)).sum(axis=1)
+    if nfr == 0:
+        return e
+    thr = e.mean()
+    for _ in range(_TA_ITERS):
+        sel = e <= thr
+        if not sel.any():
+            break
+        mu = e[sel].mean()
+        thr = 1.001 * (mu + 2.0 * math.sqrt(np.square(e[sel] - mu).mean()))
+    return np.where(e > thr, np.log(np.maximum(e, 1e-300) / max(thr, 1e-300)), 0.0)
+
+
+def _xcorr_window(a: np.ndarray, b: np.ndarray, lo: int, hi: int) -> np.ndarray:
+    """c[j - lo] = sum_k a[k] b[k + j] for lags lo <= j <= hi (zero outside the arrays)."""
+    from scipy.signal import correlate
+    n = a.shape[0]
+    full = correlate(b, a, mode="full", method="fft")  # full[j + n - 1] = sum_k a[k] b[k + j]
+    out = np.zeros(hi - lo + 1)
+    j = np.arange(lo, hi + 1)
+    ok = (j > -n) & (j < b.shape[0])
+    out[ok] = full[j[ok] + n - 1]
+    return out
+
+
+def _first_max(c: np.ndarray) -> int:
+    """Index of the first maximum above zero, or -1."""
+    i = int(np.argmax(c)) if c.size else 0
+    return i if c.size and c[i] > 0 else -1
+
+
+def time_align_row(ref: np.ndarray, deg: np.ndarray, max_delay: int) -> int:
+    r = np.asarray(ref, dtype=np.float64)
+    d = np.asarray(deg, dtype=np.float64)
+    er, ed = _ta_envelope(r), _ta_envelope(d)
+    nfr = er.shape[0]
+    M = min(-(-max_delay // _TA_FRAME), nfr - 1)
+    jc = 0
+    if M >= 0 and nfr > 0:
+        i = _first_max(_xcorr_window(er, ed, -M, M))
+        jc = i - M if i >= 0 else 0
+    d0 = _TA_FRAME * jc
+    L = r.shape[0]
+    wr = np.zeros(L)
+    wd = np.zeros(L)
+    wr[1:] = np.diff(r)
+    wd[1:] = np.diff(d)
+    i = _first_max(_xcorr_window(wr, wd, d0 - _TA_FINE, d0 + _TA_FINE))
+    return d0 - _TA_FINE + i if i >= 0 else d0
+
+
+def time_align(clean: torch.Tensor, noisy: torch.Tensor, lengths=None, max_delay: int = 16000):
+    """(aligned noisy [B, L] float32, delays [B] int32) of 16 kHz rows (rows past lengths[b] 0)."""
+    c = clean.detach().cpu().numpy()
+    n = noisy.detach().cpu().numpy()
+    B, L = c.shape
+    out = np.zeros((B, L), dtype=np.float32)
+    ds = np.zeros(B, dtype=np.int32)
+    for b in range(B):
+        m = L if lengths is None else int(min(max(int(lengths[b]), 0), L))
+        D = time_align_row(c[b, :m], n[b, :m], max_delay)
+        ds[b] = D
+        lo, hi = max(0, -D), min(m, m - D)
+        if hi > lo:
+            out[b, lo:hi] = n[b, lo + D:hi + D]
+    return torch.from_numpy(out), torch.from_numpy(ds)

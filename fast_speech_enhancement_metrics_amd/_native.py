@@ -54,6 +54,9 @@ SIGNATURES = {
     "fsem_stoi_tob_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_i64, _vp, _c_sz, _vp]),
     "fsem_pesq_stoi_workspace_bytes": (_c_sz, [_c_i64, _c_i64]),
     "fsem_pesq_stoi_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _c_sz, _vp]),
+    "fsem_time_align_workspace_bytes": (_c_sz, [_c_i64, _c_i64]),
+    "fsem_time_align_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _c_i32, _vp, _vp, _c_i64, _vp,
+                                            _c_sz, _vp]),
 }
 
 

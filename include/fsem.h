@@ -183,6 +183,28 @@ int fsem_pesq_stoi_f32(const float *ref, const float *deg, int64_t batch, int64_
                        int64_t ld, const int32_t *lengths, float *mos, float *stoi, float *estoi,
                        void *ws, size_t ws_bytes, void *stream);
 
+/* ---------------------------------------------------------------- time alignment (opt-in)
+ * NOT in the reference, whose PESQ has no time alignment (fast_se_metrics/PESQ.py:19-22); the
+ * PESQ(..., time_align=True) extension calls this before the PESQ entries.
+ * Per row pair of 16 kHz signals, after ITU-T P.862 section 10 (restated in
+ * oracle/align_oracle.py; parity against P.862 implementations unpinned):
+ *   crude delay from 4 ms voice-activity log envelopes (|delay| <= max_delay samples, rounded
+ *   up to 4 ms frames), then the sample lag within +-383 of it maximising the cross-correlation
+ *   of the signals' first differences.  delay[b] = D > 0: deg lags ref, deg[n] ~ ref[n - D].
+ *   ref, deg    : [batch, length] float32 (row stride ld, ld % 4 == 0, 16-byte aligned rows)
+ *   lengths     : NULL or [batch] int32 per-row lengths (Conventions)
+ *   delay       : NULL or [batch] int32 output (at least one of delay / deg_aligned)
+ *   deg_aligned : NULL or [batch, length] float32 output (row stride ld_out):
+ *                 deg_aligned[b][n] = deg[b][n + D] where 0 <= n + D < lengths[b], else 0
+ *                 (not in place: deg_aligned must not overlap deg)
+ * Cost: about 767 multiply-adds per sample (the fine search); see csrc/align.hip.
+ */
+size_t fsem_time_align_workspace_bytes(int64_t batch, int64_t length);
+int fsem_time_align_f32(const float *ref, const float *deg, int64_t batch, int64_t length,
+                        int64_t ld, const int32_t *lengths, int32_t max_delay, int32_t *delay,
+                        float *deg_aligned, int64_t ld_out, void *ws, size_t ws_bytes,
+                        void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -15,6 +15,6 @@ if [ -n "$REV" ]; then
 fi
 C=$SRC/fast_speech_enhancement_metrics_amd/csrc
 /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -shared -fPIC -Wno-unused-result ${EXTRA:-} \
-  -o "$OUT/$NAME.so" "$C/pesq.hip" "$C/stoi.hip" "$C/resample.hip"
+  -o "$OUT/$NAME.so" "$C/pesq.hip" "$C/stoi.hip" "$C/resample.hip" $([ -f "$C/align.hip" ] && echo "$C/align.hip")
 [ -n "$REV" ] && rm -rf "$SRC"
 echo "$OUT/$NAME.so"
