@@ -56,7 +56,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=5)
     ap.add_argument("--separate", action="store_true", help="two API calls (PESQ, STOI) instead of the joint entry")
-    ap.add_argument("--workload", default="c2", choices=["c2", "pesq", "c3", "c5"],
+    ap.add_argument("--workload", default="c2", choices=["c2", "pesq", "pesq_aligned", "c3", "c5"],
                     help="c2: BASELINE metric (default, PESQ-wb + STOI/ESTOI); pesq: configs[1] as stated, "
                          "PESQ-wb only; c3: STOI+ESTOI only, 8192 x 5 s @ 16 kHz per GPU; "
                          "c5: config 5, mixed 8/16 kHz ragged 2-30 s batch")
@@ -322,22 +322,40 @@ def run_pesq(args, world, rank, dev, distributed):
     from fast_speech_enhancement_metrics_amd.synthetic import speech_like_pairs
     B, L = 4096, 160000
     clean, noisy, _ = speech_like_pairs(B, L, 16000, seed=42 + rank, device=dev)
-    pesq = PESQ(16000, use_gpu=True)
+    aligned = args.workload == "pesq_aligned"
+    if aligned:
+        # extension (not in the reference): degraded rows delayed by U[-2000, 2000] samples,
+        # PESQ(time_align=True) estimates and undoes the delay before scoring (alignment.py)
+        g = torch.Generator(device=dev)
+        g.manual_seed(7 + rank)
+        delay = torch.randint(-2000, 2001, (B,), generator=g, device=dev)
+        src = torch.arange(L, device=dev)[None, :] - delay[:, None]
+        noisy = torch.where((src >= 0) & (src < L), noisy.gather(1, src.clamp(0, L - 1)), torch.zeros_like(noisy))
+        del src
+    pesq = PESQ(16000, use_gpu=True, time_align=aligned)
 
     def step():
         p = pesq.scores(clean, noisy)
         return p.cpu() if rank == 0 else None
 
     dt = _timed(step, args, dev, distributed)
+    if aligned:
+        found = int((pesq.last_delays.long() == delay).sum())
     if rank == 0:
-        print(json.dumps({
-            "metric": "utterances/sec PESQ-wb, 10s@16kHz, batch 4096 (config 2)",
+        line = {
+            "metric": ("utterances/sec PESQ-wb with time alignment (extension), 10s@16kHz, batch 4096" if aligned
+                       else "utterances/sec PESQ-wb, 10s@16kHz, batch 4096 (config 2)"),
             "value": round(world * B * args.steps / dt, 2), "unit": "utterances/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic speech-like pairs",
-            "config": {"workload": "config 2: PESQ-wb scores (PESQ.scores)", "batch_per_gpu": B, "length": L,
-                       "sample_rate": 16000, "parallelism": f"dp{world}"}}), flush=True)
+            "data": "synthetic speech-like pairs" + (", degraded rows delayed by U[-2000, 2000] samples" if aligned
+                                                     else ""),
+            "config": {"workload": ("PESQ(16000, use_gpu=True, time_align=True).scores" if aligned
+                                    else "config 2: PESQ-wb scores (PESQ.scores)"), "batch_per_gpu": B,
+                       "length": L, "sample_rate": 16000, "parallelism": f"dp{world}"}}
+        if aligned:
+            line["delays_recovered"] = f"{found}/{B}"
+        print(json.dumps(line), flush=True)
 
 
 def run_c5(args, world, rank, dev, distributed):
@@ -435,8 +453,9 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    if args.workload in ("pesq", "c3", "c5"):
-        {"pesq": run_pesq, "c3": run_c3, "c5": run_c5}[args.workload](args, world, rank, dev, distributed)
+    if args.workload in ("pesq", "pesq_aligned", "c3", "c5"):
+        {"pesq": run_pesq, "pesq_aligned": run_pesq, "c3": run_c3, "c5": run_c5}[args.workload](
+            args, world, rank, dev, distributed)
         if distributed:
             dist.barrier()
             dist.destroy_process_group()

@@ -53,7 +53,7 @@ def time_align(clean: torch.Tensor, noisy: torch.Tensor, lengths=None,
         pad = (-L) % 4  # 16-byte aligned rows read in 16-byte pieces, one stride (include/fsem.h)
         c = torch.nn.functional.pad(c, (0, pad)).contiguous()
         n = torch.nn.functional.pad(n, (0, pad)).contiguous()
-    out = torch.empty(B, L, dtype=torch.float32, device=c.device)
+    out = torch.empty(B, L + (-L) % 4, dtype=torch.float32, device=c.device)[:, :L]  # float4 row stores
     delays = torch.empty(B, dtype=torch.int32, device=c.device)
     ws = _native.workspace(lib.fsem_time_align_workspace_bytes(B, L), c.device)
     _native.check(lib.fsem_time_align_f32(c.data_ptr(), n.data_ptr(), B, L, c.stride(0),

@@ -13,7 +13,7 @@
 // Delay D > 0: the degraded row lags the clean one, deg[n] ~ ref[n - D].
 //
 // Cost is set by stage 3: 767 lags x L multiply-adds per row (about 123 M for 10 s), as
-// register-blocked FMAs out of LDS (16 consecutive lags per lane sliding over the chunk);
+// register-blocked packed FMAs out of LDS (16 consecutive lags per lane sliding over the chunk);
 // the other stages are O(L) or O(M * L / 64).
 #include "fsem_common.h"
 
@@ -24,10 +24,10 @@ constexpr int FRAME = 64;            // envelope frame (4 ms at 16 kHz)
 constexpr int VAD_ITERS = 12;
 constexpr int FINE = 383;            // fine half-width in samples
 constexpr int NLAG = 2 * FINE + 1;   // 767
-constexpr int LG = 16;               // lags per lane
-constexpr int NGRP = 48;             // lag groups (48 x 16 = 768 slots >= NLAG)
-constexpr int NSL = 5;               // sample slices per chunk
-constexpr int SL = 1024;             // samples per slice
+constexpr int LG = 32;               // lags per lane
+constexpr int NGRP = 24;             // lag groups (24 x 32 = 768 slots >= NLAG)
+constexpr int NSL = 10;              // sample slices per chunk
+constexpr int SL = 512;              // samples per slice
 constexpr int CS = NSL * SL;         // samples per chunk (5120)
 constexpr int WIN = CS + NGRP * LG;  // degraded window per chunk (5888)
 static_assert(NGRP * LG >= NLAG && NGRP * NSL <= 256, "fine-stage thread map");
@@ -39,9 +39,9 @@ __device__ __forceinline__ int64_t row_len(const int32_t *lengths, int64_t b, in
   return n < 0 ? 0 : (n > L ? L : n);
 }
 
-// LDS index of the degraded window's element m: a one-float skew every 16 so the 48 lag groups
-// of a wave (16 floats apart) read distinct banks.
-__device__ __forceinline__ int skew(int m) { return m + (m >> 4); }
+// LDS index of the degraded window's element m: a one-float skew every 32 so the 24 lag groups
+// of a wave (32 floats apart) read distinct banks.
+__device__ __forceinline__ int skew(int m) { return m + (m >> 5); }
 
 // ---------------------------------------------------------------- stage 1: frame energies
 // 16 lanes per frame (one float4 each), 4 frames per wave; frames of row s: k < L_row / 64.
@@ -170,7 +170,7 @@ __global__ void __launch_bounds__(256) ta_crude(int64_t B, int64_t L, const int3
 // Workgroup (row b, chunk c): samples n in [c CS, (c+1) CS).  First differences in LDS:
 // wr[n] (n >= 1, n < L_row), wd[m] for m = n + D over the window D in [D0 - FINE, D0 - FINE + 768).
 // Thread (slice sl, group g): 16 lags D0 - FINE + 16 g + i over its 1024 samples, the window
-// wd[n + lag0 + i] held in registers and slid one sample per step (unrolled by 16: no moves).
+// wd[n + lag0 + i] held in registers as even- and odd-aligned pairs, two samples per step.
 // Partials per lag over the chunk: the five slices added in order, to part[b][c][768].
 __global__ void __launch_bounds__(256) ta_fine_partial(const float *__restrict__ ref, const float *__restrict__ deg,
                                                        int64_t B, int64_t L, int64_t ld,
@@ -178,7 +178,7 @@ __global__ void __launch_bounds__(256) ta_fine_partial(const float *__restrict__
                                                        const int *__restrict__ crude, int nchunk,
                                                        float *__restrict__ part) {
   __shared__ float wr[CS];
-  __shared__ float wd[WIN + WIN / 16 + 16];
+  __shared__ float wd[WIN + WIN / 32 + 64];
   __shared__ float ps[NSL][NGRP * LG];
   const int64_t blk = blockIdx.x;
   const int64_t b = blk / nchunk;
@@ -193,29 +193,48 @@ __global__ void __launch_bounds__(256) ta_fine_partial(const float *__restrict__
     return (i >= 1 && i < Lr) ? z[i] - z[i - 1] : 0.f;
   };
   for (int i = tid; i < CS; i += 256) wr[i] = dif(x, n0 + i);
-  for (int i = tid; i < WIN; i += 256) wd[skew(i)] = dif(y, n0 + lag0 + i);
+  for (int i = tid; i < WIN + 32; i += 256) wd[skew(i)] = dif(y, n0 + lag0 + i);  // +32: last slides
   __syncthreads();
   const int g = tid % NGRP, sl = tid / NGRP;
   if (sl < NSL) {
-    float acc[LG], w[LG];
+    // packed FP32 (v_pk_fma_f32: two lags per instruction).  W[i] = the window element of lag
+    // LG g + i at the current sample; E[p] = (W[2p], W[2p+1]) serves the even sample of a
+    // double step, O[p] = (W[2p+1], W[2p+2]) the odd one.  A double step retires the logical
+    // pair 0 of both and appends the pairs (W[LG], W[LG+1]) / (W[LG+1], W[LG+2]): physical slot
+    // (p + k) % (LG/2) holds logical pair p in double step k (unrolled: no moves but the
+    // append).  Per double step: LG packed FMAs, two window reads, half a float4 of wr.
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    constexpr int NP = LG / 2;
+    f2 acc[NP], E[NP], O[NP];
+    const int base = SL * sl + LG * g;
 #pragma unroll
-    for (int i = 0; i < LG; ++i) {
-      acc[i] = 0.f;
-      w[i] = wd[skew(SL * sl + LG * g + i)];  // lag (16 g + i), sample SL sl
+    for (int p = 0; p < NP; ++p) {
+      acc[p] = (f2){0.f, 0.f};
+      const float a = wd[skew(base + 2 * p)], b1 = wd[skew(base + 2 * p + 1)], b2 = wd[skew(base + 2 * p + 2)];
+      E[p] = (f2){a, b1};
+      O[p] = (f2){b1, b2};
     }
-    const float *rr = wr + SL * sl;
+    const float4 *rr4 = reinterpret_cast<const float4 *>(wr + SL * sl);
     for (int n = 0; n < SL; n += LG) {
 #pragma unroll
-      for (int u = 0; u < LG; ++u) {
-        const float xr = rr[n + u];
+      for (int k = 0; k < NP; ++k) {
+        const int sm = n + 2 * k;
+        const float4 xq = rr4[sm >> 2];  // the same float4 for two double steps (CSE)
+        const float x0 = (k & 1) ? xq.z : xq.x, x1 = (k & 1) ? xq.w : xq.y;
 #pragma unroll
-        for (int i = 0; i < LG; ++i) acc[i] = fmaf(xr, w[(u + i) % LG], acc[i]);
-        // slide: the slot of w[u] now takes the element LG ahead (sample n + u + 1, lag 16 g + 15)
-        w[u] = wd[skew(SL * sl + n + u + LG + LG * g)];
+        for (int p = 0; p < NP; ++p) acc[p] = __builtin_elementwise_fma((f2){x0, x0}, E[(p + k) % NP], acc[p]);
+#pragma unroll
+        for (int p = 0; p < NP; ++p) acc[p] = __builtin_elementwise_fma((f2){x1, x1}, O[(p + k) % NP], acc[p]);
+        const float wa = wd[skew(base + sm + LG + 1)], wb = wd[skew(base + sm + LG + 2)];
+        E[k] = (f2){O[(NP - 1 + k) % NP].y, wa};
+        O[k] = (f2){wa, wb};
       }
     }
 #pragma unroll
-    for (int i = 0; i < LG; ++i) ps[sl][LG * g + i] = acc[i];
+    for (int p = 0; p < NP; ++p) {
+      ps[sl][LG * g + 2 * p] = acc[p].x;
+      ps[sl][LG * g + 2 * p + 1] = acc[p].y;
+    }
   }
   __syncthreads();
   for (int j = tid; j < NGRP * LG; j += 256) {
@@ -264,16 +283,28 @@ __global__ void __launch_bounds__(256) ta_fine_pick(int64_t B, const int *__rest
 }
 
 // ---------------------------------------------------------------- stage 4: shift
+// Four outputs per thread (one float4 store; ld_out % 4 == 0), four scalar reads at n + D.
 __global__ void __launch_bounds__(256) ta_shift(const float *__restrict__ deg, int64_t B, int64_t L, int64_t ld,
                                                 const int32_t *__restrict__ lengths, const int *__restrict__ delay,
                                                 float *__restrict__ out, int64_t ld_out) {
   const int64_t b = blockIdx.y + (int64_t)blockIdx.z * 65535;
   if (b >= B) return;
-  const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t n = 4 * ((int64_t)blockIdx.x * 256 + threadIdx.x);
   if (n >= L) return;
   const int64_t Lr = row_len(lengths, b, L);
-  const int64_t m = n + delay[b];
-  out[b * ld_out + n] = (n < Lr && m >= 0 && m < Lr) ? deg[b * ld + m] : 0.f;
+  const int64_t D = delay[b];
+  const float *y = deg + b * ld;
+  float v[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t m = n + i + D;
+    v[i] = (n + i < Lr && m >= 0 && m < Lr) ? y[m] : 0.f;
+  }
+  if (n + 4 <= L) {
+    *reinterpret_cast<float4 *>(out + b * ld_out + n) = make_float4(v[0], v[1], v[2], v[3]);
+  } else {
+    for (int i = 0; i < 4 && n + i < L; ++i) out[b * ld_out + n + i] = v[i];
+  }
 }
 
 inline int64_t frames_cap(int64_t L) { return L / FRAME; }
@@ -320,7 +351,7 @@ extern "C" int fsem_time_align_f32(const float *ref, const float *deg, int64_t b
                                    const int32_t *lengths, int32_t max_delay, int32_t *delay, float *deg_aligned,
                                    int64_t ld_out, void *ws, size_t ws_bytes, void *stream) {
   if (!ref || !deg || batch <= 0 || length <= 0 || ld < length || length > kMaxLength || max_delay < 0 ||
-      (deg_aligned && ld_out < length) || (!delay && !deg_aligned) || (ld % 4) != 0)
+      (deg_aligned && (ld_out < length || ld_out % 4 != 0)) || (!delay && !deg_aligned) || (ld % 4) != 0)
     return FSEM_EINVAL;
   const int64_t nch = align::nchunks(length);
   if (batch * nch > INT32_MAX) return FSEM_EINVAL;
@@ -350,7 +381,7 @@ extern "C" int fsem_time_align_f32(const float *ref, const float *deg, int64_t b
   FSEM_CHECK_LAUNCH();
   if (deg_aligned) {
     dim3 grid = yz(batch);
-    grid.x = (unsigned)((length + 255) / 256);
+    grid.x = (unsigned)((length + 1023) / 1024);
     align::ta_shift<<<grid, 256, 0, st>>>(deg, batch, length, ld, lengths, dl, deg_aligned, ld_out);
     FSEM_CHECK_LAUNCH();
   }

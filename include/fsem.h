@@ -194,7 +194,8 @@ int fsem_pesq_stoi_f32(const float *ref, const float *deg, int64_t batch, int64_
  *   ref, deg    : [batch, length] float32 (row stride ld, ld % 4 == 0, 16-byte aligned rows)
  *   lengths     : NULL or [batch] int32 per-row lengths (Conventions)
  *   delay       : NULL or [batch] int32 output (at least one of delay / deg_aligned)
- *   deg_aligned : NULL or [batch, length] float32 output (row stride ld_out):
+ *   deg_aligned : NULL or [batch, length] float32 output (row stride ld_out, ld_out % 4 == 0,
+ *                 16-byte aligned rows):
  *                 deg_aligned[b][n] = deg[b][n + D] where 0 <= n + D < lengths[b], else 0
  *                 (not in place: deg_aligned must not overlap deg)
  * Cost: about 767 multiply-adds per sample (the fine search); see csrc/align.hip.
