@@ -11,5 +11,6 @@ from .base import BaseMetric
 from .PESQ import PESQ
 from .STOI import STOI
 from .joint import PESQ_STOI
+from .alignment import time_align
 
-__all__ = ["BaseMetric", "PESQ", "STOI", "PESQ_STOI"]
+__all__ = ["BaseMetric", "PESQ", "STOI", "PESQ_STOI", "time_align"]

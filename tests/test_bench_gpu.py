@@ -46,3 +46,24 @@ def test_bench_gpus_beyond_visible_fails():
     out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(n), "--steps", "1"],
                          cwd=REPO, capture_output=True, text=True, timeout=120)
     assert out.returncode != 0 and "visible" in out.stderr and out.stdout.strip() == ""
+
+
+def test_bench_rccl_path_one_rank_pipelined():
+    """The driver's multi-GPU launch form (torch.distributed.run, RCCL) with one rank, at a batch
+    where the drop-in call pipelines two 2048-row chunks (joint.py pipeline_rows) and the scores
+    are all-gathered: one JSON line, n_gpus 1."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                          "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(REPO, "bench.py"),
+                          "--gpus", "1", "--batch", "4096", "--length", "16000", "--steps", "2", "--warmup", "1",
+                          "--kernel-reps", "1", "--no-cpu-baseline"],
+                         cwd=REPO, capture_output=True, text=True, timeout=240, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.strip().startswith("{")]
+    assert len(lines) == 1, out.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 1 and d["value"] > 0 and d["config"]["batch_per_gpu"] == 4096
