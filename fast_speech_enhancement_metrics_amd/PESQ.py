@@ -252,7 +252,7 @@ class PESQ(BaseMetric):
         lib = _native.load() if clean.is_cuda else None
         if lib is None:
             if lengths is None:
-                return _cpu.pesq(clean, noisy)
+                return _cpu.rows_parallel(_cpu.pesq, clean, noisy)
             return _cpu.per_row(_cpu.pesq, clean, noisy, device_lengths(lengths, B, L, "cpu"))
         F = lib.fsem_pesq_frames(L)
         lens = device_lengths(lengths, B, L, clean.device) if lengths is not None else None

