@@ -356,10 +356,10 @@ def time_align(clean: torch.Tensor, noisy: torch.Tensor, lengths=None, max_delay
     B, L = c.shape
     out = np.zeros((B, L), dtype=np.float32)
     ds = np.zeros(B, dtype=np.int32)
+    rows = [L if lengths is None else int(min(max(int(lengths[b]), 0), L)) for b in range(B)]
+    ds[:] = _host_map(lambda b: time_align_row(c[b, :rows[b]], n[b, :rows[b]], max_delay), range(B))
     for b in range(B):
-        m = L if lengths is None else int(min(max(int(lengths[b]), 0), L))
-        D = time_align_row(c[b, :m], n[b, :m], max_delay)
-        ds[b] = D
+        m, D = rows[b], int(ds[b])
         lo, hi = max(0, -D), min(m, m - D)
         if hi > lo:
             out[b, lo:hi] = n[b, lo + D:hi + D]

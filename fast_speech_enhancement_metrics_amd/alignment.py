@@ -40,6 +40,7 @@ def time_align(clean: torch.Tensor, noisy: torch.Tensor, lengths=None,
         raise Exception("`clean_speech` and `denoised_speech` should have the same shape.")
     if max_delay < 0:
         raise ValueError("max_delay must be >= 0")
+    max_delay = min(int(max_delay), 2**31 - 1)  # the C-ABI's int32
     B, L = c.shape
     if not c.is_cuda:
         lens = None if lengths is None else device_lengths(lengths, B, L, "cpu")
