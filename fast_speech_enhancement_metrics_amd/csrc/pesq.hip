@@ -7,8 +7,8 @@
 // with two kernels:
 //
 // pesq_front  persistent 256-thread workgroups over items (signal, segment of 48 frames):
-//   A  float4 buffer loads of a 13 312-sample tile (768 warm-up + 48 hops + 1 hop) into LDS,
-//      prefetched in registers during the previous item's FFT phase
+//   A  float4 buffer loads of a 13 312-sample tile (768 warm-up + 48 hops + 1 hop) into LDS
+//      at the item's start (the other resident workgroup covers their latency)
 //   J  (joint entry only) STOI's 16 -> 10 kHz resampler on the same tile, on MFMA, plus the
 //      STOI VAD quarter sums of the clean rows (see resample_tile)
 //   B  level-alignment band-pass power (PESQ.py:92-98), time-parallel:
@@ -82,11 +82,11 @@ constexpr int XBUF = SCAN_B0 + PT * 13;                        // 7040 floats
 static_assert(XBUF >= 4 * 2 * kFftBuf, "FFT exchange areas fit");
 constexpr int SPEC_LD = 258;      // parked spectrum row stride: = 2 mod 32, MFMA A reads conflict-free
 constexpr int NBP = 10;           // band-pass states
-constexpr int PF = TILE / 4 / PT; // float4 per thread per tile (prefetch registers)
+constexpr int PF = TILE / 4 / PT; // float4 per thread per tile
 static_assert(WARM + 256 * (NF + 1) == TILE, "tile geometry");
 static_assert(SCAN_LD == 13 && 64 * SCAN_LD <= SCAN_A_WAVE, "scan buffer A: a wave's states within its staging slice");
 static_assert(SPEC_LD * (NF - 1) + 256 <= TILE, "parked spectra stay in the tile");
-static_assert(TILE % (4 * PT) == 0, "prefetch split");
+static_assert(TILE % (4 * PT) == 0, "tile load split");
 
 // Bark bands are stored band-major per signal: bark[(s * NBARK + k) * bark_ld(F) + f], rows
 // padded to a multiple of 32 frames: every row starts on a 128-byte line, so the back end's
@@ -190,12 +190,18 @@ __device__ __forceinline__ Item make_item(int64_t item, int nseg, int64_t B, int
   return it;
 }
 
-// Issue the global loads of one tile into registers (consumed one item later).  Raw buffer
-// loads with a wave-uniform descriptor over [0, ceil4(L)): out-of-range float4s (t < 0 wraps
-// the 32-bit offset; t >= ceil4(L)) return zeros from the hardware range check.  Samples in
+// One tile straight into LDS: buffer loads with the LDS as destination (buffer_load_dwordx4 ...
+// lds: 16 bytes per lane to the wave-uniform base in M0 + 16 lane), no VGPRs, no LDS stores.
+// A wave-uniform descriptor over [0, ceil4(L)): out-of-range float4s (t < 0 wraps the 32-bit
+// offset; t >= ceil4(L)) arrive as zeros from the hardware range check.  Samples in
 // [L, ceil4(L)) may hold anything: both filters are causal and every output at t >= L is
-// masked, so they cannot reach a result (rows must be readable up to ceil4(L), include/fsem.h).
-__device__ __forceinline__ void prefetch(const Item &it, int tid, float4 pre[PF]) {
+// masked, so they cannot reach a PESQ result (rows must be readable up to ceil4(L),
+// include/fsem.h); the joint resampler zeroes them (below).  The caller waits (vmcnt) and
+// barriers before reading the tile.  Measured in round 3: loading the next item's tile into
+// registers during the FFT / Bark phases (a prefetch, 52 VGPRs held across them) was slower
+// than loading at the item's start (5.27 vs 5.21 ms): the second resident workgroup hides the
+// latency, and the prefetch registers cost spills and scheduling.
+__device__ __forceinline__ void load_tile_lds(const Item &it, int tid, float *tile) {
   const int64_t L = it.L;
   const uint64_t base = reinterpret_cast<uint64_t>(it.xrow);
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base);
@@ -204,12 +210,12 @@ __device__ __forceinline__ void prefetch(const Item &it, int tid, float4 pre[PF]
   void *p = reinterpret_cast<void *>(((uint64_t)hi << 32) | lo);
   const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(p, 0, nbytes, 0x00020000);
   const int t0 = (int)it.tstart;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 #pragma unroll
   for (int k = 0; k < PF; ++k) {
     const int t = t0 + 4 * (tid + PT * k);
-    typedef float v4f __attribute__((ext_vector_type(4)));
-    const v4f v = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(rsrc, t * 4, 0, 0));
-    pre[k] = make_float4(v.x, v.y, v.z, v.w);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+        rsrc, (__attribute__((address_space(3))) void *)(tile + 4 * (64 * wave + PT * k)), 16, t * 4, 0, 0, 0);
   }
 }
 
@@ -624,13 +630,8 @@ __global__ void __launch_bounds__(PT, 2)
   auto item_at = [&](int64_t i) {
     return SAFE ? (int64_t)rlist[i / nseg] * nseg + i % nseg : i;
   };
-  float4 pre[PF];
-  int64_t item = blockIdx.x;
-  if (!SAFE && item < n_items) prefetch(make_item(item_at(item), nseg, B, ld, Lcap, lens, ref, deg), tid, pre);
-
-  for (; item < n_items; item += gridDim.x) {
+  for (int64_t item = blockIdx.x; item < n_items; item += gridDim.x) {
     const Item it = make_item(item_at(item), nseg, B, ld, Lcap, lens, ref, deg);
-    if (SAFE) prefetch(it, tid, pre);  // no pipelining in the rare pass
     const int64_t L = it.L;
     Geometry rg;  // this row's geometry (the launch's for uniform batches)
     if (VARLEN) {
@@ -642,31 +643,17 @@ __global__ void __launch_bounds__(PT, 2)
     }
     if (VARLEN && it.g >= rg.nseg) {  // segment past this row's end: no samples, no frames
       if (tid < 4) ppart[(it.s * nseg + it.g) * 4 + tid] = 0.f;
-      const int64_t nxt = item + gridDim.x;
-      if (!SAFE && nxt < n_items) prefetch(make_item(item_at(nxt), nseg, B, ld, Lcap, lens, ref, deg), tid, pre);
       continue;
     }
     STAMP(0);
-    {
-      float4 *t4 = reinterpret_cast<float4 *>(tile);
-      if (JOINT && it.tstart + TILE > L) {  // the row ends in this tile: the resampler sees zeros
-#pragma unroll                               // past it (torchaudio pads, base.py:20)
-        for (int k = 0; k < PF; ++k) {
-          float4 v = pre[k];
-          const int t = (int)(it.tstart - (L & ~(int64_t)3)) + 4 * (tid + PT * k);  // vs ceil4 start
-          if (t >= 0) {
-            const int r = (int)(L & 3);  // valid samples in the float4 that starts at floor4(L)
-            v.x = (t == 0 && r > 0) ? v.x : 0.f;
-            v.y = (t == 0 && r > 1) ? v.y : 0.f;
-            v.z = (t == 0 && r > 2) ? v.z : 0.f;
-            v.w = 0.f;
-          }
-          t4[tid + PT * k] = v;
-        }
-      } else {
-#pragma unroll
-        for (int k = 0; k < PF; ++k) t4[tid + PT * k] = pre[k];
-      }
+    load_tile_lds(it, tid, tile);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's tile loads have landed
+    if (JOINT && (L & 3) && it.tstart + TILE > L) {
+      // the row ends in this tile: the resampler sees zeros past it (torchaudio pads,
+      // base.py:20); only the float4 at floor4(L) holds samples past L (the rest is range-checked)
+      lds_barrier();
+      const int r = (int)(L & 3), q = (int)((L & ~(int64_t)3) - it.tstart);
+      if (tid < 4 && tid >= r && q >= 0) tile[q + tid] = 0.f;
     }
     lds_barrier();
     STAMP(14);
@@ -826,12 +813,6 @@ __global__ void __launch_bounds__(PT, 2)
     }
     lds_barrier();
     STAMP(4);
-    // issue the next item's tile loads now: they stay in flight through the FFT / Bark
-    // phases (the IIR phases above run without the prefetch registers live)
-    if (!SAFE) {
-      const int64_t nxt = item + gridDim.x;
-      if (nxt < n_items) prefetch(make_item(item_at(nxt), nseg, B, ld, Lcap, lens, ref, deg), tid, pre);
-    }
 
     // ---------------------------------------------------------------- FFT rounds
     const int nfr = min(NF, rg.F - g * NF);  // valid frames in this segment
