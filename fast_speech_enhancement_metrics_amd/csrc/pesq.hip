@@ -818,46 +818,58 @@ __global__ void __launch_bounds__(PT, 2)
     const int nfr = min(NF, rg.F - g * NF);  // valid frames in this segment
     float2 *wbuf = reinterpret_cast<float2 *>(xbuf) + wave * kFftBuf;
     const int nrounds = nfr > 0 ? (nfr + 7) / 8 : 0;
-    for (int rd = 0; rd < nrounds; ++rd) {
-      const int fa = 2 * (4 * rd + wave);
-      float pa[4], pb[4];
-      const bool active = fa < nfr;
-      if (active) {
-        cf v[8];
-        const float *fra = tile + WARM + 256 * fa;
+    // RPB rounds per barrier: their spectra are held (8 RPB values per lane) until every wave
+    // has read the tile for them, then parked; the parking of rounds rd .. rd+RPB-1 stays below
+    // the inputs of round rd+RPB (258 (8 rd + 8 RPB) <= 768 + 2048 (rd + RPB))
+    constexpr int RPB = 3;
+    static_assert(SPEC_LD * 8 * RPB <= WARM + 256 * 8 * RPB && SPEC_LD * NF <= WARM + 256 * NF,
+                  "parking below the next rounds' inputs");
+    for (int rd = 0; rd < nrounds; rd += RPB) {
+      float pa[RPB][4], pb[RPB][4];
 #pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          const int n = lane + 64 * r;
-          v[r] = {fra[n] * win[r], fra[256 + n] * win[r]};
-        }
-        fft512_wave(v, wbuf, lane, tw1, tw2);
+      for (int h = 0; h < RPB; ++h) {
+        const int fa = 2 * (4 * (rd + h) + wave);
+        if (fa < nfr) {
+          cf v[8];
+          const float *fra = tile + WARM + 256 * fa;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float mr = __shfl(v[7 - r].r, plane, 64);
-          float mi = __shfl(v[7 - r].i, plane, 64);
-          if (lane == 0) {
-            mr = v[(8 - r) & 7].r;
-            mi = v[(8 - r) & 7].i;
+          for (int r = 0; r < 8; ++r) {
+            const int n = lane + 64 * r;
+            v[r] = {fra[n] * win[r], fra[256 + n] * win[r]};
           }
-          const float zr = v[r].r, zi = v[r].i;
-          // 4 |Z_a|^2, 4 |Z_b|^2: the 1/4 is folded into the Bark weights (bcor)
-          pa[r] = fmaf(zr + mr, zr + mr, (zi - mi) * (zi - mi));  // explicit: no contraction choice
-          pb[r] = fmaf(zi + mi, zi + mi, (zr - mr) * (zr - mr));
-        }
-        if (lane == 0) {  // spec[:, :, 0] = 0 (PESQ.py:136)
-          pa[0] = 0.f;
-          pb[0] = 0.f;
+          fft512_wave(v, wbuf, lane, tw1, tw2);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float mr = __shfl(v[7 - r].r, plane, 64);
+            float mi = __shfl(v[7 - r].i, plane, 64);
+            if (lane == 0) {
+              mr = v[(8 - r) & 7].r;
+              mi = v[(8 - r) & 7].i;
+            }
+            const float zr = v[r].r, zi = v[r].i;
+            // 4 |Z_a|^2, 4 |Z_b|^2: the 1/4 is folded into the Bark weights (bcor)
+            pa[h][r] = fmaf(zr + mr, zr + mr, (zi - mi) * (zi - mi));  // explicit: no contraction choice
+            pb[h][r] = fmaf(zi + mi, zi + mi, (zr - mr) * (zr - mr));
+          }
+          if (lane == 0) {  // spec[:, :, 0] = 0 (PESQ.py:136)
+            pa[h][0] = 0.f;
+            pb[h][0] = 0.f;
+          }
         }
       }
-      lds_barrier();  // every wave is done reading the tile for this round
+      lds_barrier();  // every wave is done reading the tile for these rounds
       STAMP(6 + rd);
-      if (active) {  // park the spectra in the consumed part of the tile
-        float *ra = tile + SPEC_LD * fa;
-        float *rb = ra + SPEC_LD;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          ra[lane + 64 * r] = pa[r];
-          rb[lane + 64 * r] = pb[r];
+      for (int h = 0; h < RPB; ++h) {
+        const int fa = 2 * (4 * (rd + h) + wave);
+        if (fa < nfr) {  // park the spectra in the consumed part of the tile
+          float *ra = tile + SPEC_LD * fa;
+          float *rb = ra + SPEC_LD;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            ra[lane + 64 * r] = pa[h][r];
+            rb[lane + 64 * r] = pb[h][r];
+          }
         }
       }
     }
