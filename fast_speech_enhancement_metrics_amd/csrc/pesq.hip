@@ -547,7 +547,7 @@ __device__ __forceinline__ void resample_tile(const float *__restrict__ tile, in
 }
 
 // Persistent: each workgroup walks items (signal, segment) = blockIdx.x, +gridDim.x, ...;
-// the next item's tile is in flight in registers while the current one is processed.
+// each item's tile goes straight into LDS at its start (load_tile_lds).
 // rng: the range bookkeeping in the workspace -- pexp [2B * nseg] (per-segment shifts, zeroed
 // before the main pass), count [1], flags [2B] (zeroed), worklist [2B] of flagged signals.
 // SAFE (JOINT = false only): process the worklist's signals' segments with range shifts.
