@@ -94,3 +94,19 @@ def test_bench_size_recovers_every_delay(dev):
     assert (ds.long() == D).all(), int((ds.long() != D).sum())
     for b in (0, 1, 200, 511):
         assert int(ds[b]) == A.delay(c[b].cpu().numpy(), deg[b].cpu().numpy())
+
+
+def test_pesq_time_align_ragged_rows(dev):
+    """PESQ(time_align=True) with per-row lengths: each row aligned within its own length, then
+    scored as that row alone (the engine's PESQ of the oracle-aligned rows, bitwise)."""
+    from fast_speech_enhancement_metrics_amd import PESQ
+    c, deg, D = _delayed(6, 48000, 35, 2000)
+    lens = np.array([48000, 40000, 36001, 47999, 30000, 44444], dtype=np.int32)
+    ct, dt = torch.from_numpy(c).to(dev), torch.from_numpy(deg).to(dev)
+    lt = torch.from_numpy(lens).to(dev)
+    m = PESQ(16000, use_gpu=True, time_align=True)
+    got = m.scores(ct, dt, lengths=lt).cpu().numpy()
+    oal, ods = A.align(c, deg, lengths=lens)
+    np.testing.assert_array_equal(m.last_delays.cpu().numpy(), ods)
+    want = PESQ(16000, use_gpu=True).scores(ct, torch.from_numpy(oal).to(dev), lengths=lt).cpu().numpy()
+    np.testing.assert_array_equal(got, want)
