@@ -21,7 +21,7 @@ B, L = int(os.environ.get("B", "4096")), 160000
 c, n, _ = speech_like_pairs(B, L, 16000, seed=42, device="cuda")
 _vp, _i64, _sz = ctypes.c_void_p, ctypes.c_int64, ctypes.c_size_t
 SEGS = [("tile->LDS", 0, 14), ("resample", 14, 1), ("IIR pass1", 1, 2), ("scan", 2, 3), ("IIR pass2", 3, 4),
-        ("fft r0", 4, 6)] + [(f"fft r{r}", 5 + r, 6 + r) for r in range(1, 6)] + [("bark (to end)", 11, 15)]
+        ("FFT rounds", 4, 13), ("bark", 13, 15)]
 rows = {}
 for v in sys.argv[1:]:
     lib = ctypes.CDLL(os.path.join(os.path.dirname(__file__), "..", "fast_speech_enhancement_metrics_amd", "lib",
