@@ -915,4 +915,4 @@ extern "C" const char *fsem_strerror(int code) {
   }
 }
 
-extern "C" int fsem_version(void) { return 2; }
+extern "C" int fsem_version(void) { return 3; }  // 3: + fsem_time_align_*, fsem_pesq_distances_*

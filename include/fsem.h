@@ -58,7 +58,7 @@ extern "C" {
 #define FSEM_ERATE -5         /* unsupported sample-rate pair (see resampling)      */
 
 const char *fsem_strerror(int code);
-int fsem_version(void);
+int fsem_version(void);  /* 3 since round 3 (time alignment and distances entries) */
 
 /* ---------------------------------------------------------------- resampling
  * torchaudio.transforms.Resample(orig, new) (sinc_interp_hann, width 6,
