@@ -149,10 +149,12 @@ def cpu_baseline(clean, noisy, batches=(4, 64), calls=7):
             "batches": {str(b): v for b, v in out.items()}}
 
 
-def kernel_roofline(clean, noisy, reps, joint):
+def kernel_roofline(clean, noisy, reps, joint, config_batch=None):
     """HIP-event timing of the dominant kernel -- pesq_front, launched alone through its stage
     entry (fsem_pesq_front_y10_f32 for the joint path, fsem_pesq_front_f32 otherwise) -- on the
-    stream it is launched on; achieved = algorithmic bytes per launch / avg duration."""
+    stream it is launched on, over the rows one engine call of the step processes (the drop-in
+    call's chunk: 2048 of the 4096 rows); achieved = algorithmic bytes per launch / avg duration.
+    `config_batch`: the bench configuration's batch (the PMC summaries are recorded at it)."""
     from fast_speech_enhancement_metrics_amd import _native
     lib = _native.load()
     B, L = clean.shape
@@ -214,12 +216,18 @@ FRONT_KERNELS = {True: ("pesq_front<true, false, false>", "pesq_front<true, fals
                  False: ("pesq_front<false, false, false>", "pesq_front<false, false>")}
 
 
+def _pmc_meta_ok(d: dict, rows: int, L: int) -> bool:
+    """A summary recorded at `rows` x `L` per engine call ("_meta"; older summaries: 4096 x 160000)."""
+    m = d.get("_meta", {"rows_per_launch": 4096, "length": 160000})
+    return (m.get("rows_per_launch"), m.get("length")) == (rows, L)
+
+
 def pmc_counter(kernel, counter: str, B: int, L: int):
     """(value per launch, source) of one counter of `kernel` (a name suffix, or a tuple of them)
-    from the newest committed PMC summary."""
+    from the newest committed PMC summary recorded at B rows x L samples per launch."""
     import glob
     import re
-    if (B, L) != (4096, 160000):
+    if L != 160000:
         return None
 
     def natural(path):
@@ -232,7 +240,7 @@ def pmc_counter(kernel, counter: str, B: int, L: int):
         except (OSError, ValueError):
             continue
         key = next((k for k in d if k.endswith(kernel)), None)
-        if key and counter in d[key]:
+        if key and counter in d[key] and _pmc_meta_ok(d, B, L):
             best = (int(d[key][counter]), os.path.relpath(f, HERE))
     return best
 
@@ -240,10 +248,11 @@ def pmc_counter(kernel, counter: str, B: int, L: int):
 def pmc_traffic(kernel, B: int, L: int):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
     (profiles/*/pmc_summary.json, tools/pmc_summary.py: FETCH_SIZE x2 gfx950 correction +
-    WRITE_SIZE, MI355X_MICROARCH.md 'HBM'), recorded at this same configuration; the counters
-    need their own rocprofv3 passes, so they cannot be read inside the timed run."""
+    WRITE_SIZE, MI355X_MICROARCH.md 'HBM'), recorded at this same per-launch size (B rows x L
+    samples); the counters need their own rocprofv3 passes, so they cannot be read inside the
+    timed run."""
     import glob
-    if (B, L) != (4096, 160000):
+    if L != 160000:
         return None, None
     best = None
     import re
@@ -257,7 +266,7 @@ def pmc_traffic(kernel, B: int, L: int):
         except (OSError, ValueError):
             continue
         key = next((k for k in d if k.endswith(kernel)), None)
-        if key and "hbm_bytes" in d[key]:
+        if key and "hbm_bytes" in d[key] and _pmc_meta_ok(d, B, L):
             best = (int(d[key]["hbm_bytes"]), os.path.relpath(f, HERE))
     return best if best else (None, None)
 
@@ -486,16 +495,23 @@ def main():
             gather_scores(local_scores, world * B)
         return res
 
+    # the drop-in call's engine calls (row chunks; joint.chunk_bounds): the scores path and the
+    # roofline launch the kernels at the same per-call size, so every pesq_front launch of this
+    # command has one size and rocprofv3's average is the roofline's launch
+    bounds = joint.chunk_bounds(B, True) if not args.separate else [(0, B)]
+    launch_rows = max(hi - lo for lo, hi in bounds)
+
     def scores_step():
-        # engine API alone: scores on the device, one device->host copy
-        p, s, e = joint.scores(clean, noisy)
-        local = torch.stack([p, s, e], dim=1)
+        # engine API alone: scores on the device (the same row chunks), one device->host copy
+        parts = [torch.stack(joint.scores(clean[lo:hi], noisy[lo:hi]), dim=1) for lo, hi in bounds]
+        local = parts[0] if len(parts) == 1 else torch.cat(parts)
         full = gather_scores(local, world * B) if distributed else local
         return full.cpu() if rank == 0 else None
 
     # the dominant kernel's roofline (HIP-event timed launches of its stage entry) first: the
     # GPU's clocks are still ramping during the first steps after the input generation
-    roof = kernel_roofline(clean, noisy, args.kernel_reps, joint=not args.separate)
+    roof = kernel_roofline(clean[:launch_rows], noisy[:launch_rows], args.kernel_reps, joint=not args.separate,
+                           config_batch=B)
     dt = _timed(step, args, dev, distributed)
     ms_per_step = dt / args.steps * 1e3
     value = world * B * args.steps / dt

@@ -110,7 +110,8 @@ class PESQ_STOI(BaseMetric):
         with torch.inference_mode():
             rows = torch.atleast_2d(denoised_speech)
             B = rows.shape[0]
-            K = B // self.pipeline_rows if (rows.is_cuda and self.pipeline_rows > 0) else 1
+            bounds = self.chunk_bounds(B, rows.is_cuda)
+            K = len(bounds)
             if K <= 1:
                 out = torch.stack([t.float() for t in self.scores(clean_speech, denoised_speech, lengths,
                                                                   sample_rate=16000)])
@@ -120,7 +121,6 @@ class PESQ_STOI(BaseMetric):
                 lens = None if lengths is None else device_lengths(lengths, B, rows.shape[-1], rows.device)
                 pinned = self._pinned(3 * B)
                 stream = torch.cuda.current_stream(rows.device)
-                bounds = [(k * B // K, (k + 1) * B // K) for k in range(K)]
                 parts, done = [], []
                 for lo, hi in bounds:
                     part = torch.stack([t.float() for t in self.scores(
@@ -139,6 +139,14 @@ class PESQ_STOI(BaseMetric):
         if all(d["STOI"] != d["STOI"] for d in res):  # as STOI (STOI.py:162-165)
             warnings.warn("Not enough non-silent frames. Please check your sound files", RuntimeWarning, stacklevel=4)
         return res, out.t()
+
+    def chunk_bounds(self, batch: int, on_gpu: bool = True) -> list[tuple[int, int]]:
+        """Row ranges of the engine calls the drop-in call makes for `batch` rows: one range, or
+        batch // pipeline_rows consecutive ones on the GPU (bench.py times the dominant kernel and
+        the scores path at this per-call size, so every launch in the bench has one size)."""
+        K = batch // self.pipeline_rows if (on_gpu and self.pipeline_rows > 0) else 1
+        K = max(K, 1)
+        return [(k * batch // K, (k + 1) * batch // K) for k in range(K)]
 
     def _pinned(self, n: int) -> torch.Tensor:
         """A pinned host float32 buffer of at least n elements, kept across calls.  A call waits for

@@ -37,12 +37,17 @@ def test_cpu_oracle_fields():
 
 
 def test_roofline_traffic_from_newest_pmc_summary():
-    hbm, src = bench.pmc_traffic(bench.FRONT_KERNELS[True], 4096, 160000)
-    assert hbm is not None and hbm > 5_242_880_000  # at least the algorithmic input bytes
     rounds = sorted(os.listdir(os.path.join(REPO, "profiles")),
                     key=lambda p: [int(t) if t.isdigit() else t for t in __import__("re").split(r"(\d+)", p)])
     newest = [r for r in rounds if os.path.exists(os.path.join(REPO, "profiles", r, "pmc_summary.json"))][-1]
+    with open(os.path.join(REPO, "profiles", newest, "pmc_summary.json")) as f:
+        rows = json.load(f).get("_meta", {"rows_per_launch": 4096})["rows_per_launch"]
+    hbm, src = bench.pmc_traffic(bench.FRONT_KERNELS[True], rows, 160000)
+    assert hbm is not None and hbm > 2 * rows * 160000 * 4  # at least the algorithmic input bytes
     assert src == os.path.join("profiles", newest, "pmc_summary.json")
+    other = 2048 if rows == 4096 else 4096  # a summary is only used at its own per-launch size
+    got = bench.pmc_traffic(bench.FRONT_KERNELS[True], other, 160000)
+    assert got == (None, None) or got[1] != src
     assert bench.pmc_traffic(bench.FRONT_KERNELS[True], 64, 160000) == (None, None)  # other sizes: none
 
 

@@ -5,7 +5,9 @@
 Per fsem kernel, averaged over its launches: raw counter values, plus HBM bytes corrected as
 MI355X_MICROARCH.md 'HBM' prescribes: FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950
 FETCH_SIZE counts half the bytes of wide (16 B/lane) coalesced streaming reads, so
-hbm_read_bytes = 2 * 1024 * FETCH_SIZE; hbm_write_bytes = 1024 * WRITE_SIZE.
+hbm_read_bytes = 2 * 1024 * FETCH_SIZE; hbm_write_bytes = 1024 * WRITE_SIZE.  "_meta" records the
+rows and length of one profiled engine call (env PMC_ROWS / PMC_LENGTH, set by the drivers);
+bench.py only takes counters recorded at its own per-launch size.
 """
 import collections
 import csv
@@ -38,6 +40,9 @@ def main(root: str):
         if "hbm_read_bytes" in d and "hbm_write_bytes" in d:
             d["hbm_bytes"] = d["hbm_read_bytes"] + d["hbm_write_bytes"]
         out[k] = d
+    # the engine call the passes profiled (tools/one_step.py: the drop-in call's row chunk)
+    out["_meta"] = {"rows_per_launch": int(os.environ.get("PMC_ROWS", "4096")),
+                    "length": int(os.environ.get("PMC_LENGTH", "160000"))}
     json.dump(out, sys.stdout, indent=1, sort_keys=True)
     print()
 
