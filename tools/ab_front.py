@@ -1,7 +1,8 @@
 """Interleaved A/B of the PESQ front end across library variants in ONE process (GPU box):
 every variant's fsem_pesq_front_y10_f32 (the joint front end, as bench.py's roofline times it)
 is launched `--reps` times per round on the same inputs, HIP-event timed on the current stream,
-over `--rounds` rounds in rotating order; prints the median per variant.
+over `--rounds` rounds in rotating order; prints the median per variant and whether its Bark
+bands and powers are bitwise those of the first variant.
 
     python tools/ab_front.py va vb ...     (libraries fast_speech_enhancement_metrics_amd/lib/var/NAME.so)
 """
@@ -76,6 +77,14 @@ for r in range(a.rounds):
         e1.record()
         e1.synchronize()
         times[v].append(e0.elapsed_time(e1) / a.reps)
+outs = {}
+for v in libs:  # outputs of each variant (the same inputs): bitwise comparison with the first
+    launch(libs[v])
+    torch.cuda.synchronize()
+    outs[v] = (bark.clone(), power.clone())
+first = next(iter(outs))
 for v in libs:
     t = times[v]
-    print(f"{v}: median {statistics.median(t):.4f} ms  min {min(t):.4f}  max {max(t):.4f}  ({len(t)} rounds)")
+    same = all(torch.equal(a, b) for a, b in zip(outs[v], outs[first]))
+    print(f"{v}: median {statistics.median(t):.4f} ms  min {min(t):.4f}  max {max(t):.4f}  ({len(t)} rounds)"
+          f"  bark/power bitwise equal to {first}: {same}")
