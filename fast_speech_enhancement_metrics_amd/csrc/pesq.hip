@@ -669,6 +669,7 @@ __global__ void __launch_bounds__(PT, 2)
   auto item_at = [&](int64_t i) {
     return SAFE ? (int64_t)rlist[i / nseg] * nseg + i % nseg : i;
   };
+  bool prefetched = false;  // this item's tile load went out during the previous item's Bark phase
   for (int64_t item = blockIdx.x; item < n_items; item += gridDim.x) {
     const Item it = make_item(item_at(item), nseg, B, ld, Lcap, lens, ref, deg);
     const int64_t L = it.L;
@@ -682,10 +683,12 @@ __global__ void __launch_bounds__(PT, 2)
     }
     if (VARLEN && it.g >= rg.nseg) {  // segment past this row's end: no samples, no frames
       if (tid < 4) ppart[(it.s * nseg + it.g) * 4 + tid] = 0.f;
+      if (prefetched) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // its unused tile load (ordered before the next)
+      prefetched = false;
       continue;
     }
     STAMP(0);
-    load_tile_lds(it, tid, tile);
+    if (!prefetched) load_tile_lds(it, tid, tile);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's tile loads have landed
     if (JOINT && (L & 3) && it.tstart + TILE > L) {
       // the row ends in this tile: the resampler sees zeros past it (torchaudio pads,
@@ -863,19 +866,30 @@ __global__ void __launch_bounds__(PT, 2)
     constexpr int RPB = 3;
     static_assert(SPEC_LD * 8 * RPB <= WARM + 256 * 8 * RPB && SPEC_LD * NF <= WARM + 256 * NF,
                   "parking below the next rounds' inputs");
+    // the 12 distinct tile samples of a frame pair (frame a: [0, 512), frame b: [256, 768))
+    auto load_pair = [&](int fa, float o[12]) {
+      const float *fra = tile + WARM + 256 * fa;  // in the tile for every fa < 2 (4 * 6)
+#pragma unroll
+      for (int r = 0; r < 12; ++r) o[r] = fra[lane + 64 * r];
+    };
+    static_assert(WARM + 256 * (2 * (4 * (RPB * ((NF / 8 + RPB - 1) / RPB) - 1) + 3)) + 768 <= TILE + TILE_PAD,
+                  "frame-pair reads of every round stay in the tile");
     for (int rd = 0; rd < nrounds; rd += RPB) {
       float pa[RPB][4], pb[RPB][4];
+      float cur[12];
+      load_pair(2 * (4 * rd + wave), cur);
 #pragma unroll
       for (int h = 0; h < RPB; ++h) {
         const int fa = 2 * (4 * (rd + h) + wave);
+        // the next pair's samples are read before this pair's FFT, their LDS latency hidden
+        // behind its butterflies (measured 2.534 -> 2.521 ms per 2048-row launch; reading the
+        // next barrier group's first pair too spills VGPRs: 2.572)
+        float nxt[12];
+        if (h + 1 < RPB) load_pair(2 * (4 * (rd + h + 1) + wave), nxt);
         if (fa < nfr) {
           cf v[8];
-          const float *fra = tile + WARM + 256 * fa;
 #pragma unroll
-          for (int r = 0; r < 8; ++r) {
-            const int n = lane + 64 * r;
-            v[r] = {fra[n] * win[r], fra[256 + n] * win[r]};
-          }
+          for (int r = 0; r < 8; ++r) v[r] = {cur[r] * win[r], cur[r + 4] * win[r]};
           fft512_wave(v, wbuf, lane, tw1, tw2);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
@@ -894,6 +908,10 @@ __global__ void __launch_bounds__(PT, 2)
             pa[h][0] = 0.f;
             pb[h][0] = 0.f;
           }
+        }
+        if (h + 1 < RPB) {
+#pragma unroll
+          for (int r = 0; r < 12; ++r) cur[r] = nxt[r];
         }
       }
       lds_barrier();  // every wave is done reading the tile for these rounds
@@ -949,38 +967,53 @@ __global__ void __launch_bounds__(PT, 2)
             if (fl + i < nfr) o[i] = v[i];
         }
       };
+      // The tile is free once every wave has read its last A operands: the next item's tile
+      // load goes out then, before the last MFMA batch and the stores (which cover part of its
+      // latency).  Waves 0-2 hold tile 2's last 29 K-steps across the barrier, wave 3 frame tile 2.
+      auto next_tile = [&]() {
+        lds_barrier();  // every wave holds its remaining operands: the tile may be rewritten
+        prefetched = false;
+        if (item + gridDim.x < n_items) {
+          const Item nit = make_item(item_at(item + gridDim.x), nseg, B, ld, Lcap, lens, ref, deg);
+          load_tile_lds(nit, tid, tile);
+          prefetched = true;
+        }
+      };
       if (wave < 3) {
-        if (16 * wave < nfr) {
-          const float *srow = tile + SPEC_LD * min(16 * wave + row, nfr - 1);
-          f4 c0 = {0.f, 0.f, 0.f, 0.f}, c2a = c0, c2b = c0;
+        constexpr int KB1 = 16, KR = (K2b - K2a) - KB1;  // tile 2: first batch, the rest
+        const bool act = 16 * wave < nfr;
+        // operands read and MFMAs run unconditionally (rows clamped into the tile; results of a
+        // frame tile past nfr are not stored): no partially defined registers across the barrier
+        const float *srow = tile + SPEC_LD * min(16 * wave + row, max(nfr, 1) - 1);
+        f4 c0 = {0.f, 0.f, 0.f, 0.f}, c2a = c0, c2b = c0;
+        auto mf2 = [&](int j, float a) {
+          const float bv = j < 32 ? bop(bm2lo, j, bcor[2]) : bop(bm2hi, j - 32, bcor[2]);
+          if (j & 1)
+            c2b = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bv, c2b, 0, 0, 0);
+          else
+            c2a = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bv, c2a, 0, 0, 0);
+        };
+        float ar[KR];
+        {
           // A operand: the wave's 16 spectrum rows, one bin per lane per K-step; a batch's LDS
           // reads are issued before its MFMA chain (the chain then never waits on LDS latency)
-          {
-            float a0[K0b - K0a];
+          float a0[K0b - K0a], a2[KB1];
 #pragma unroll
-            for (int k = 0; k < K0b - K0a; ++k) a0[k] = srow[4 * (K0a + k) + kq];
+          for (int k = 0; k < K0b - K0a; ++k) a0[k] = srow[4 * (K0a + k) + kq];
 #pragma unroll
-            for (int k = 0; k < K0b - K0a; ++k)
-              c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[k], bop(bm013, k, bcor[0]), c0, 0, 0, 0);
-          }
-          constexpr int KB = 16;  // tile 2 in batches of 16 K-steps, two accumulators
+          for (int k = 0; k < KB1; ++k) a2[k] = srow[4 * (K2a + k) + kq];
 #pragma unroll
-          for (int k0 = K2a; k0 < K2b; k0 += KB) {
-            float a2[KB];
+          for (int k = 0; k < K0b - K0a; ++k)
+            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[k], bop(bm013, k, bcor[0]), c0, 0, 0, 0);
 #pragma unroll
-            for (int k = 0; k < KB; ++k) a2[k] = (k0 + k < K2b) ? srow[4 * (k0 + k) + kq] : 0.f;
+          for (int k = 0; k < KR; ++k) ar[k] = srow[4 * (K2a + KB1 + k) + kq];
 #pragma unroll
-            for (int k = 0; k < KB; ++k) {
-              if (k0 + k < K2b) {
-                const int j = k0 + k - K2a;
-                const float bv = j < 32 ? bop(bm2lo, j, bcor[2]) : bop(bm2hi, j - 32, bcor[2]);
-                if (k & 1)
-                  c2b = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[k], bv, c2b, 0, 0, 0);
-                else
-                  c2a = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[k], bv, c2a, 0, 0, 0);
-              }
-            }
-          }
+          for (int k = 0; k < KB1; ++k) mf2(k, a2[k]);
+        }
+        next_tile();
+#pragma unroll
+        for (int k = 0; k < KR; ++k) mf2(KB1 + k, ar[k]);
+        if (act) {
           put4(row, 16 * wave + 4 * kq, c0);
           put4(32 + row, 16 * wave + 4 * kq, c2a + c2b);
         }
@@ -992,24 +1025,29 @@ __global__ void __launch_bounds__(PT, 2)
           c3[f] = c1[f];
         }
         // three frame tiles = three independent accumulator chains per band tile
+        float a1[3][K1b - K1a], a3[3][K3b - K3a];
+        auto rd = [&](int f) {
+          const float *srow = tile + SPEC_LD * min(16 * f + row, max(nfr, 1) - 1);
 #pragma unroll
-        for (int f = 0; f < 3; ++f) {
-          if (16 * f < nfr) {
-            const float *srow = tile + SPEC_LD * min(16 * f + row, nfr - 1);
-            float a1[K1b - K1a], a3[K3b - K3a];
+          for (int k = 0; k < K1b - K1a; ++k) a1[f][k] = srow[4 * (K1a + k) + kq];
 #pragma unroll
-            for (int k = 0; k < K1b - K1a; ++k) a1[k] = srow[4 * (K1a + k) + kq];
+          for (int k = 0; k < K3b - K3a; ++k) a3[f][k] = srow[4 * (K3a + k) + kq];
+        };
+        auto mf = [&](int f) {
 #pragma unroll
-            for (int k = 0; k < K3b - K3a; ++k) a3[k] = srow[4 * (K3a + k) + kq];
+          for (int k = 0; k < K1b - K1a; ++k)
+            c1[f] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[f][k], bop(bm013, k + (K0b - K0a), bcor[1]), c1[f], 0, 0, 0);
 #pragma unroll
-            for (int k = 0; k < K1b - K1a; ++k)
-              c1[f] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[k], bop(bm013, k + (K0b - K0a), bcor[1]), c1[f], 0, 0, 0);
+          for (int k = 0; k < K3b - K3a; ++k)
+            c3[f] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                a3[f][k], bop(bm013, k + (K0b - K0a) + (K1b - K1a), bcor[3]), c3[f], 0, 0, 0);
+        };
 #pragma unroll
-            for (int k = 0; k < K3b - K3a; ++k)
-              c3[f] = __builtin_amdgcn_mfma_f32_16x16x4f32(
-                  a3[k], bop(bm013, k + (K0b - K0a) + (K1b - K1a), bcor[3]), c3[f], 0, 0, 0);
-          }
-        }
+        for (int f = 0; f < 3; ++f) rd(f);
+        mf(0);
+        mf(1);
+        next_tile();
+        mf(2);
 #pragma unroll
         for (int f = 0; f < 3; ++f) {
           if (16 * f < nfr) {
@@ -1019,7 +1057,6 @@ __global__ void __launch_bounds__(PT, 2)
         }
       }
     }
-    lds_barrier();  // tile is rewritten by the next item
     STAMP(15);
   }
 }
