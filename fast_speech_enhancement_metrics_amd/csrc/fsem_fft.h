@@ -105,6 +105,18 @@ __device__ __forceinline__ void dft8v_lo4(f2 v[8]) {
   v[7] = FSEM_FMA2(t3, nh, b3);
 }
 
+// v[r] *= tw[r] for r = 1..7 as cmul2 in two sweeps: the seven products first, then the seven
+// fused multiply-adds, so no v_pk_fma_f32 directly follows the v_pk_mul_f32 it reads (gfx950
+// inserts a wait state between a packed-FP32 result and its packed reader: one s_nop per pair
+// when the compiler keeps each pair together).  Same operations per element as cmul2.
+__device__ __forceinline__ void twiddle7(f2 v[8], const cf tw[8]) {
+  f2 t[8];
+#pragma unroll
+  for (int r = 1; r < 8; ++r) t[r] = v[r].xx * (f2){tw[r].r, tw[r].i};
+#pragma unroll
+  for (int r = 1; r < 8; ++r) v[r] = FSEM_FMA2((f2){tw[r].i, tw[r].r}, (f2){-v[r].y, v[r].y}, t[r]);
+}
+
 // 512-point complex FFT of one wave, radix-8 Stockham, natural-order result in
 // v[r] = Z[lane + 64 r].  `buf` = this wave's kFftBuf-float2 LDS exchange area.
 // LO4: Z[n] = 0 for n >= 256 (vc[4..7] are not read).
@@ -126,8 +138,7 @@ __device__ __forceinline__ void fft512_wave(cf vc[8], float2 *buf, int lane, con
     float2 t = buf[fpad(lane + 64 * r)];
     v[r] = (f2){t.x, t.y};
   }
-#pragma unroll
-  for (int r = 1; r < 8; ++r) v[r] = cmul2(v[r], (f2){tw1[r].r, tw1[r].i});
+  twiddle7(v, tw1);
   dft8v(v);
   wave_lds_fence();
   const int o1 = (lane >> 3) * 64 + (lane & 7);
@@ -139,8 +150,7 @@ __device__ __forceinline__ void fft512_wave(cf vc[8], float2 *buf, int lane, con
     float2 t = buf[fpad(lane + 64 * r)];
     v[r] = (f2){t.x, t.y};
   }
-#pragma unroll
-  for (int r = 1; r < 8; ++r) v[r] = cmul2(v[r], (f2){tw2[r].r, tw2[r].i});
+  twiddle7(v, tw2);
   dft8v(v);
   wave_lds_fence();
 #pragma unroll

@@ -585,7 +585,8 @@ __device__ __forceinline__ void resample_tile(const float *__restrict__ tile, in
   }
 }
 
-// Persistent: each workgroup walks items (signal, segment) = blockIdx.x, +gridDim.x, ...;
+// Persistent: workgroup w starts at item (signal, segment) w and takes its further items from a
+// queue (one atomic per item, claimed an item ahead);
 // each item's tile goes straight into LDS at its start (load_tile_lds).
 // rng: the range bookkeeping in the workspace -- pexp [2B * nseg] (per-segment shifts, zeroed
 // before the main pass), count [1], flags [2B] (zeroed), worklist [2B] of flagged signals.
@@ -600,6 +601,7 @@ __global__ void __launch_bounds__(PT, 2)
   __shared__ __attribute__((aligned(16))) float tile[TILE + TILE_PAD];
   __shared__ __attribute__((aligned(16))) float xbuf[XBUF];
   __shared__ float red[8];
+  __shared__ int64_t next_item;  // the workgroup's next item (from the queue)
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar branches)
@@ -662,7 +664,10 @@ __global__ void __launch_bounds__(PT, 2)
 
   int *__restrict__ const pexp = rng;
   int *__restrict__ const rcount = rng + 2 * B * nseg;
-  int *__restrict__ const rflag = rcount + 1;
+  // items past the first gridDim.x come from a queue (counter zeroed with the range bookkeeping):
+  // a workgroup that becomes resident late (other kernels on its CU) takes fewer items
+  unsigned int *__restrict__ const qcount = reinterpret_cast<unsigned int *>(rcount + 1);
+  int *__restrict__ const rflag = rcount + 2;
   int *__restrict__ const rlist = rflag + 2 * B;
   // SAFE: the worklist's items (signal rlist[i / nseg], segment i % nseg); usually none
   const int64_t n_items = SAFE ? (int64_t)__builtin_amdgcn_readfirstlane(*rcount) * nseg : nitems;
@@ -670,7 +675,17 @@ __global__ void __launch_bounds__(PT, 2)
     return SAFE ? (int64_t)rlist[i / nseg] * nseg + i % nseg : i;
   };
   bool prefetched = false;  // this item's tile load went out during the previous item's Bark phase
-  for (int64_t item = blockIdx.x; item < n_items; item += gridDim.x) {
+  for (int64_t item = blockIdx.x, item_next; item < n_items; item = item_next) {
+    // the item after this one: claimed now (lane 0 of wave 0), published to the workgroup before
+    // the next tile load (next_tile) or at the item's end; the SAFE pass strides statically
+    unsigned int claim = 0;
+    if (!SAFE && tid == 0) claim = atomicAdd(qcount, 1u);
+    item_next = -1;
+    auto take_next = [&]() {  // every thread; a barrier between the write and the reads
+      if (tid == 0) next_item = SAFE ? item + gridDim.x : (int64_t)gridDim.x + claim;
+      lds_barrier();
+      item_next = next_item;
+    };
     const Item it = make_item(item_at(item), nseg, B, ld, Lcap, lens, ref, deg);
     const int64_t L = it.L;
     Geometry rg;  // this row's geometry (the launch's for uniform batches)
@@ -685,6 +700,8 @@ __global__ void __launch_bounds__(PT, 2)
       if (tid < 4) ppart[(it.s * nseg + it.g) * 4 + tid] = 0.f;
       if (prefetched) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // its unused tile load (ordered before the next)
       prefetched = false;
+      take_next();
+      lds_barrier();  // every thread has read next_item before it is rewritten
       continue;
     }
     STAMP(0);
@@ -971,10 +988,10 @@ __global__ void __launch_bounds__(PT, 2)
       // load goes out then, before the last MFMA batch and the stores (which cover part of its
       // latency).  Waves 0-2 hold tile 2's last 29 K-steps across the barrier, wave 3 frame tile 2.
       auto next_tile = [&]() {
-        lds_barrier();  // every wave holds its remaining operands: the tile may be rewritten
+        take_next();  // (its barrier: every wave holds its remaining operands, the tile may be rewritten)
         prefetched = false;
-        if (item + gridDim.x < n_items) {
-          const Item nit = make_item(item_at(item + gridDim.x), nseg, B, ld, Lcap, lens, ref, deg);
+        if (item_next < n_items) {
+          const Item nit = make_item(item_at(item_next), nseg, B, ld, Lcap, lens, ref, deg);
           load_tile_lds(nit, tid, tile);
           prefetched = true;
         }
@@ -1058,6 +1075,10 @@ __global__ void __launch_bounds__(PT, 2)
       }
     }
     STAMP(15);
+    if (item_next < 0) {  // no Bark phase ran (uniform)
+      take_next();
+      lds_barrier();
+    }
   }
 }
 
@@ -1423,9 +1444,9 @@ static size_t front_ppart_bytes(int64_t batch, int64_t length) {
   return align_up(sizeof(float) * (size_t)(2 * batch) * (size_t)pesq::geometry(length).nseg * 4, 256);
 }
 
-// range bookkeeping after the partials: pexp [2B nseg], count, flags [2B], worklist [2B] (int)
+// range bookkeeping after the partials: pexp [2B nseg], count, item queue, flags [2B], worklist [2B] (int)
 static size_t front_rng_ints(int64_t batch, int64_t length) {
-  return (size_t)(2 * batch) * (size_t)pesq::geometry(length).nseg + 1 + 4 * (size_t)batch;
+  return (size_t)(2 * batch) * (size_t)pesq::geometry(length).nseg + 2 + 4 * (size_t)batch;
 }
 
 extern "C" size_t fsem_pesq_front_workspace_bytes(int64_t batch, int64_t length) {
@@ -1462,8 +1483,9 @@ int fsem::pesq::launch_front(const float *ref, const float *deg, int64_t batch, 
   float *ppart = static_cast<float *>(ws);
   int *rng = reinterpret_cast<int *>(static_cast<char *>(ws) + front_ppart_bytes(batch, length));
   int *pexp = rng;
-  // shifts, worklist count and flags start at zero (the worklist itself is written before read)
-  if (hipMemsetAsync(rng, 0, sizeof(int) * ((size_t)(2 * batch) * g.nseg + 1 + 2 * (size_t)batch), st) != hipSuccess)
+  // shifts, worklist count, item queue and flags start at zero (the worklist itself is written
+  // before read)
+  if (hipMemsetAsync(rng, 0, sizeof(int) * ((size_t)(2 * batch) * g.nseg + 2 + 2 * (size_t)batch), st) != hipSuccess)
     return FSEM_ELAUNCH;
 #define FSEM_FRONT(J, V, S)                                                                                      \
   hipLaunchKernelGGL((pesq::pesq_front<J, V, S>), dim3((unsigned)grid), dim3(pesq::PT), 0, st, ref, deg, batch,  \
