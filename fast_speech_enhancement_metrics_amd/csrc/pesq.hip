@@ -684,7 +684,7 @@ __global__ void __launch_bounds__(PT, 2)
     auto take_next = [&]() {  // every thread; a barrier between the write and the reads
       if (tid == 0) next_item = SAFE ? item + gridDim.x : (int64_t)gridDim.x + claim;
       lds_barrier();
-      item_next = next_item;
+      item_next = uniform_i64(next_item);
     };
     const Item it = make_item(item_at(item), nseg, B, ld, Lcap, lens, ref, deg);
     const int64_t L = it.L;
