@@ -33,12 +33,12 @@ class PESQ(BaseMetric):
     EXPECTED_SAMPLING_RATE = 16000
 
     def __init__(self, sample_rate: int = 16000, use_gpu: bool = False, *, time_align: bool = False,
-                 max_delay: int = 16000):
+                 max_delay: int = 16000, devices=None):
         """``time_align`` (extension, off by default as in the reference, PESQ.py:19-22): shift each
         degraded row by its estimated delay before scoring (``alignment.time_align``, P.862-style;
         ``max_delay`` samples at 16 kHz bounds the search).  The delays of the last scored batch
-        are kept in ``last_delays``."""
-        super().__init__(sample_rate, use_gpu)
+        are kept in ``last_delays``.  ``devices``: see BaseMetric (multi-device calls)."""
+        super().__init__(sample_rate, use_gpu, devices=devices)
         self.time_align = bool(time_align)
         self.max_delay = int(max_delay)
         self.last_delays = None
@@ -141,19 +141,29 @@ class PESQ(BaseMetric):
         P = sum(bandpass(x)^2) / (L + 5120) / 1.04684."""
         speech = torch.atleast_2d(speech)
         L = speech.shape[1]
-        if speech.is_cuda:
+        if speech.is_cuda and _cpu.pesq_frames(L) >= 1:
             p = self._front(speech)[1]
         else:
-            p = torch.from_numpy(_cpu.bandpass_power(speech.detach().to(torch.float64).numpy()))
+            # host float64 cascade: CPU rows, and rows shorter than one 512-sample frame (the
+            # engine's front end frames what it filters; the reference filters any length)
+            p = torch.from_numpy(_cpu.bandpass_power(speech.detach().to("cpu", torch.float64).numpy()))
         gain = _cpu.level_scale(p, L).sqrt().to(speech.device, speech.dtype)
         return speech * gain[:, None]
 
     def pre_emphasize(self, speech: torch.Tensor) -> torch.Tensor:
         """Edge taper (in place on ``speech``, as the reference) and the pre-emphasis IIR
-        (PESQ.py:104-113)."""
+        (PESQ.py:104-113); float32 rows stay float32, on the GPU the filter runs on the device
+        (fsem_pre_emphasize_f32, torchaudio's float32 evaluation order)."""
         w = self.taper_weights.to(speech.device, speech.dtype)
         speech[:, :15] *= w
         speech[:, -15:] *= torch.flip(w, dims=(0,))
+        if speech.is_cuda:
+            x = as_rows(speech)
+            y = torch.empty(x.shape, dtype=torch.float32, device=x.device)
+            lib = _native.load()
+            _native.check(lib.fsem_pre_emphasize_f32(x.data_ptr(), x.shape[0], x.shape[1], x.stride(0), y.data_ptr(),
+                                                     y.stride(0), _native.stream_handle(x.device)), "pre-emphasis")
+            return y.to(speech.dtype)
         from scipy.signal import lfilter
         y = lfilter(_cpu._PRE_B, _cpu._PRE_A, speech.detach().to("cpu", torch.float64).numpy(), axis=1)
         return torch.from_numpy(y).to(speech.device, speech.dtype)
@@ -238,6 +248,24 @@ class PESQ(BaseMetric):
         sr = check_row_rate(self, sample_rate)
         if noisy_shape(clean_speech) != noisy_shape(denoised_speech):
             raise Exception("`clean_speech` and `denoised_speech` should have the same shape.")
+        aligned = getattr(self, "time_align", False)
+        if self.fans_out():
+            def shard(c, n, lk):
+                mos, delays = self._rows_scores(c, n, lk, sr)
+                return (mos, delays.to(torch.float32)) if aligned else mos
+
+            cols = self.fan_out(shard, clean_speech, denoised_speech, lengths, 2 if aligned else 1, balance=lengths)
+            if aligned:
+                self.last_delays = cols[1].to(torch.int32)
+            return cols[0]
+        mos, delays = self._rows_scores(clean_speech, denoised_speech, lengths, sr)
+        if aligned:
+            self.last_delays = delays
+        return mos
+
+    def _rows_scores(self, clean_speech, denoised_speech, lengths, sr: int):
+        """(mos [B], delays [B] or None) of rows at rate ``sr`` on their own device (one engine call)."""
+        delays = None
         if sr != self.EXPECTED_SAMPLING_RATE:
             clean_speech, denoised_speech, lengths = resample_rows(clean_speech, denoised_speech, lengths, sr,
                                                                    self.EXPECTED_SAMPLING_RATE)
@@ -248,12 +276,12 @@ class PESQ(BaseMetric):
             raise Exception("`clean_speech` and `denoised_speech` should have the same shape.")
         if getattr(self, "time_align", False):
             from .alignment import time_align
-            noisy, self.last_delays = time_align(clean, noisy, lengths, self.max_delay)
+            noisy, delays = time_align(clean, noisy, lengths, self.max_delay)
         lib = _native.load() if clean.is_cuda else None
         if lib is None:
             if lengths is None:
-                return _cpu.rows_parallel(_cpu.pesq, clean, noisy)
-            return _cpu.per_row(_cpu.pesq, clean, noisy, device_lengths(lengths, B, L, "cpu"))
+                return _cpu.rows_parallel(_cpu.pesq, clean, noisy), delays
+            return _cpu.per_row(_cpu.pesq, clean, noisy, device_lengths(lengths, B, L, "cpu")), delays
         F = lib.fsem_pesq_frames(L)
         lens = device_lengths(lengths, B, L, clean.device) if lengths is not None else None
         if F < 20 and lens is None:
@@ -270,7 +298,7 @@ class PESQ(BaseMetric):
                                            lens.data_ptr() if lens is not None else None,
                                            mos.data_ptr(), ws.data_ptr(), ws.numel(),
                                            _native.stream_handle(clean.device)), "PESQ")
-        return mos
+        return mos, delays
 
     def compute_metric(self, clean_speech: torch.Tensor | None, denoised_speech: torch.Tensor,
                        lengths=None) -> list[dict[str, float]]:

@@ -12,7 +12,7 @@ import warnings
 import torch
 
 from . import _cpu, _native
-from .base import BaseMetric, as_rows, check_row_rate, device_lengths, zero_tail
+from .base import BaseMetric, as_rows, check_row_rate, device_lengths, noisy_shape, zero_tail
 from .batching import resampled_lengths
 
 
@@ -20,8 +20,8 @@ class STOI(BaseMetric):
     higher_is_better = True
     EXPECTED_SAMPLING_RATE = 10000
 
-    def __init__(self, sample_rate: int = 10000, use_gpu: bool = False):
-        super().__init__(sample_rate, use_gpu)
+    def __init__(self, sample_rate: int = 10000, use_gpu: bool = False, *, devices=None):
+        super().__init__(sample_rate, use_gpu, devices=devices)
         self.sampling_frequency = self.EXPECTED_SAMPLING_RATE
         self.win_length = 256
         self.hop_length = self.win_length // 2
@@ -156,6 +156,15 @@ class STOI(BaseMetric):
         row b holds lengths[b] samples and scores as the reference would on the unpadded row.
         """
         sr = check_row_rate(self, sample_rate)
+        if self.fans_out():
+            if noisy_shape(clean_speech) != noisy_shape(denoised_speech):
+                raise Exception("`clean_speech` and `denoised_speech` should have the same shape.")
+            return self.fan_out(lambda c, n, lk: self._rows_scores(c, n, sr, lk), clean_speech, denoised_speech,
+                                lengths, 2, balance=lengths)
+        return self._rows_scores(clean_speech, denoised_speech, sr, lengths)
+
+    def _rows_scores(self, clean_speech, denoised_speech, sr: int, lengths):
+        """(stoi [B], estoi [B]) of rows at rate ``sr`` on their own device (one engine call)."""
         clean = as_rows(clean_speech)
         noisy = as_rows(denoised_speech)
         if noisy.shape != clean.shape:
@@ -220,8 +229,10 @@ class STOI(BaseMetric):
             clean_speech, denoised_speech, lengths = self.split_ragged(clean_speech, denoised_speech, lengths)
             if clean_speech.shape != denoised_speech.shape:
                 raise Exception("`clean_speech` and `denoised_speech` should have the same shape.")
-            clean = torch.atleast_2d(clean_speech).to(self.device)
-            noisy = torch.atleast_2d(denoised_speech).to(self.device)
+            clean = torch.atleast_2d(clean_speech)
+            noisy = torch.atleast_2d(denoised_speech)
+            if not self.fans_out():  # (a multi-device metric's shards copy their own rows)
+                clean, noisy = clean.to(self.home_device()), noisy.to(self.home_device())
             with torch.no_grad():
                 return self._finish(*self.scores(clean, noisy, self.sample_rate, lengths=lengths))
         return super().__call__(clean_speech, denoised_speech, lengths)

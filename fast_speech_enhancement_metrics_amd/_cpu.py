@@ -11,6 +11,7 @@ rows map to 0, rows far below 1e-12 to ~0, as the engine and the oracle).
 from __future__ import annotations
 
 import math
+import threading
 
 import numpy as np
 import torch
@@ -235,23 +236,54 @@ def stoi(clean: torch.Tensor, noisy: torch.Tensor):
     return out_s, out_e
 
 
+# torch's intra-op thread count is process-wide: concurrent _host_map calls (metric calls from
+# several Python threads) share one save / restore, counted under a lock -- the first call in
+# saves the caller's setting and sets 1, the last call out restores it.
+_threads_lock = threading.Lock()
+_threads_depth = 0
+_threads_saved = 1
+
+
+def _threads_enter() -> int:
+    """Pool size for a row map (the caller's thread count); torch's intra-op threads -> 1."""
+    global _threads_depth, _threads_saved
+    with _threads_lock:
+        if _threads_depth == 0:
+            _threads_saved = torch.get_num_threads()
+            torch.set_num_threads(1)
+        _threads_depth += 1
+        return _threads_saved
+
+
+def _threads_exit() -> None:
+    global _threads_depth
+    with _threads_lock:
+        _threads_depth -= 1
+        if _threads_depth == 0:
+            torch.set_num_threads(_threads_saved)
+
+
+def host_threads() -> int:
+    """torch's intra-op thread count as the caller set it (not the 1 of a row map in flight)."""
+    with _threads_lock:
+        return _threads_saved if _threads_depth > 0 else torch.get_num_threads()
+
+
 def _host_map(fn, items):
-    """[fn(item) for item in items] on up to torch.get_num_threads() host threads, torch's own
-    intra-op parallelism set to 1 meanwhile (rows are independent; scipy's filters and torch's
-    kernels release the GIL, so row chunks run concurrently: 2.5x for PESQ and 1.4x for STOI on
-    8 cores against one call with 8 intra-op threads)."""
+    """[fn(item) for item in items] on up to host_threads() host threads, torch's own intra-op
+    parallelism set to 1 meanwhile (rows are independent; scipy's filters and torch's kernels
+    release the GIL, so row chunks run concurrently: 2.5x for PESQ and 1.4x for STOI on 8 cores
+    against one call with 8 intra-op threads)."""
     items = list(items)
-    nt = min(torch.get_num_threads(), len(items))
-    if nt <= 1:
+    if min(host_threads(), len(items)) <= 1:
         return [fn(it) for it in items]
     from concurrent.futures import ThreadPoolExecutor
-    saved = torch.get_num_threads()
-    torch.set_num_threads(1)
+    nt = min(_threads_enter(), len(items))
     try:
-        with ThreadPoolExecutor(nt) as ex:
+        with ThreadPoolExecutor(max(nt, 1)) as ex:
             return list(ex.map(fn, items))
     finally:
-        torch.set_num_threads(saved)
+        _threads_exit()
 
 
 def _cat(outs):
@@ -264,7 +296,7 @@ def rows_parallel(fn, clean: torch.Tensor, noisy: torch.Tensor):
     """fn(clean, noisy) -> [B] tensor(s), computed over contiguous row chunks on the host's
     threads (one chunk per thread) and concatenated in row order."""
     B = clean.shape[0]
-    nt = max(1, min(torch.get_num_threads(), B))
+    nt = max(1, min(host_threads(), B))
     bounds = [(i * B // nt, (i + 1) * B // nt) for i in range(nt)]
     return _cat(_host_map(lambda lh: fn(clean[lh[0]:lh[1]], noisy[lh[0]:lh[1]]), bounds))
 

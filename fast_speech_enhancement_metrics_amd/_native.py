@@ -47,6 +47,7 @@ SIGNATURES = {
                                                 _vp, _c_i64, _vp, _c_sz, _vp]),
     "fsem_pesq_back_workspace_bytes": (_c_sz, [_c_i64, _c_i64]),
     "fsem_pesq_back_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _vp, _vp, _vp, _c_sz, _vp]),
+    "fsem_pre_emphasize_f32": (ctypes.c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _c_i64, _vp]),
     "fsem_pesq_distances_workspace_bytes": (_c_sz, [_c_i64, _c_i64]),
     "fsem_pesq_distances_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _c_sz, _vp]),
     "fsem_stoi_workspace_bytes": (_c_sz, [_c_i64, _c_i64, _c_i32]),
@@ -60,31 +61,66 @@ SIGNATURES = {
 }
 
 
-_score_list_mod = None
+_score_list_mod = None  # the native builder's module; False: unavailable, the Python form is used
 
 
-def score_list(scores, keys: tuple) -> list:
-    """[{keys[k]: scores[k][b]} for b in range(B)] from a C-contiguous float32 [K, B] host array
-    (numpy, or a CPU tensor) -- the drop-in call's result list, built natively
-    (csrc/score_list.c; compiled by _build.build_score_list, built here on first use if absent)."""
+def score_list_py(scores, keys: tuple) -> list:
+    """Python form of the native list builder (same result, same argument checks): a dict per
+    column of the [K, B] float32 / float64 scores."""
+    if not isinstance(keys, tuple):
+        raise TypeError("score_list: keys must be a tuple")
+    if not keys:
+        raise ValueError("score_list: keys must be a non-empty tuple")
+    if not all(isinstance(k, str) for k in keys):
+        raise TypeError("score_list: keys must be str")
+    import numpy as np
+    a = np.asarray(scores)
+    if a.dtype not in (np.float32, np.float64) or a.size % len(keys):
+        raise TypeError("score_list: scores must be a contiguous float32 / float64 buffer of K x B values")
+    return [dict(zip(keys, col)) for col in zip(*a.reshape(len(keys), -1).tolist())]
+
+
+def _load_score_list():
+    """The native builder (csrc/score_list.c, compiled by _build.build_score_list on first use if
+    absent), or False where it cannot be built or loaded -- no C compiler or Python headers, a
+    read-only package directory, FSEM_SCORE_LIST=python: the drop-in calls then build their lists
+    in Python (score_list_py), with a warning once."""
     global _score_list_mod
-    mod = _score_list_mod
-    if mod is None:
-        import importlib.machinery
-        import importlib.util
+    with _lock:
+        if _score_list_mod is None:
+            if os.environ.get("FSEM_SCORE_LIST") == "python":
+                _score_list_mod = False
+                return False
+            try:
+                import importlib.machinery
+                import importlib.util
 
-        from . import _build
-        with _lock:
-            if _score_list_mod is None:
+                from . import _build
                 path = _build.build_score_list()
                 loader = importlib.machinery.ExtensionFileLoader("_score_list", path)
                 spec = importlib.util.spec_from_file_location("_score_list", path, loader=loader)
                 m = importlib.util.module_from_spec(spec)
                 loader.exec_module(m)
                 _score_list_mod = m
-        mod = _score_list_mod
+            except Exception as exc:  # noqa: BLE001 -- any build / load failure: the Python form
+                import warnings
+                warnings.warn(f"native score-list builder unavailable ({exc!r}); building result lists in Python",
+                              RuntimeWarning, stacklevel=3)
+                _score_list_mod = False
+    return _score_list_mod
+
+
+def score_list(scores, keys: tuple) -> list:
+    """[{keys[k]: scores[k][b]} for b in range(B)] from a C-contiguous float32 [K, B] host array
+    (numpy, or a CPU tensor) -- the drop-in call's result list, built natively
+    (csrc/score_list.c), or by score_list_py where the native builder is unavailable."""
+    mod = _score_list_mod
+    if mod is None:
+        mod = _load_score_list()
     if isinstance(scores, torch.Tensor):
         scores = scores.detach().cpu().contiguous().numpy()
+    if mod is False:
+        return score_list_py(scores, keys)
     return mod.score_list(scores, keys)
 
 

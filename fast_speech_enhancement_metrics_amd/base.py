@@ -21,21 +21,50 @@ class BaseMetric(ABC):
     higher_is_better: bool
     EXPECTED_SAMPLING_RATE: int
 
-    def __init__(self, sample_rate: int = 16000, use_gpu: bool = False):
+    def __init__(self, sample_rate: int = 16000, use_gpu: bool = False, *, devices=None):
+        """``devices`` (extension; GPU only): None = the current device, as the reference; ``"all"``,
+        a count, or a list of devices (repeats allowed) = each call's rows split over those
+        devices from this one process (multidevice.py), scores returned on the first."""
         self.sample_rate = sample_rate
         self.device = "cuda" if use_gpu else "cpu"
         self.resampler = Resample(sample_rate, self.EXPECTED_SAMPLING_RATE)
         self.resampler.to(self.device)
+        self.devices = None
+        self._fanout = None
         if use_gpu:
             if not torch.cuda.is_available():
                 raise RuntimeError("use_gpu=True but no HIP device is visible")
             _native.load()
+            from .multidevice import FanOut, resolve_devices
+            self.devices = resolve_devices(devices)
+            if self.devices is not None:  # (one listed device: its own thread and stream alike)
+                self._fanout = FanOut(self.devices)
+
+    def home_device(self):
+        """Where results live: the first listed device of a multi-device metric, else ``.device``."""
+        return self.device if self.devices is None else self.devices[0]
+
+    def fan_out(self, score, clean, noisy, lengths, ncols: int, balance=None):
+        """``score(clean_rows, noisy_rows, lengths_rows)`` over this metric's devices (multidevice.py)
+        -> ncols [B] float32 tensors on the first listed device."""
+        return self._fanout.run(score, torch.atleast_2d(clean), torch.atleast_2d(noisy), lengths, ncols,
+                                balance_lengths=balance)
+
+    def fans_out(self) -> bool:
+        """This call's rows go to several devices (a multi-device metric, not already on a shard)."""
+        if self._fanout is None:
+            return False
+        from .multidevice import in_shard
+        return not in_shard()
 
     def prepare_audio(self, audio: torch.Tensor, lengths: torch.Tensor | None = None) -> torch.Tensor:
         """The reference's prepare_audio (base.py:16-21); with ``lengths`` each row is resampled as
-        its unpadded self (Resample.forward)."""
+        its unpadded self (Resample.forward).  A multi-device metric leaves rows at the expected
+        rate where they are: each shard copies its own rows to its device."""
         audio = torch.atleast_2d(audio)
-        audio = audio.to(self.device)
+        if self.fans_out() and self.sample_rate == self.EXPECTED_SAMPLING_RATE:
+            return audio
+        audio = audio.to(self.home_device())
         if self.sample_rate != self.EXPECTED_SAMPLING_RATE:
             audio = self.resampler(audio, lengths)
         return audio

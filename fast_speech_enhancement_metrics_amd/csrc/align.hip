@@ -169,9 +169,14 @@ __global__ void __launch_bounds__(256) ta_crude(int64_t B, int64_t L, const int3
 // ---------------------------------------------------------------- stage 3: fine partials
 // Workgroup (row b, chunk c): samples n in [c CS, (c+1) CS).  First differences in LDS:
 // wr[n] (n >= 1, n < L_row), wd[m] for m = n + D over the window D in [D0 - FINE, D0 - FINE + 768).
-// Thread (slice sl, group g): 16 lags D0 - FINE + 16 g + i over its 1024 samples, the window
-// wd[n + lag0 + i] held in registers as even- and odd-aligned pairs, two samples per step.
-// Partials per lag over the chunk: the five slices added in order, to part[b][c][768].
+// Thread (slice sl < NSL, group g < NGRP; 240 of the 256 lanes): LG = 32 lags
+// D0 - FINE + LG g + i over its SL = 512 samples, the window wd[n + lag0 + i] held in registers
+// as even- and odd-aligned pairs, two samples per step.  Partials per lag over the chunk: the
+// NSL = 10 slices added in order, to part[b][c][768].
+// Static LDS: wr (20 KB) + wd (24 KB) + ps (30 KB) = 74 KB per workgroup -- above the 64 KB
+// of earlier CDNA parts; gfx950's 160 KB LDS per CU holds two such workgroups.
+constexpr size_t kFineLds = sizeof(float) * (CS + (WIN + WIN / 32 + 64) + NSL * NGRP * LG);
+static_assert(kFineLds <= 80 * 1024, "ta_fine_partial: two workgroups per CU in gfx950's 160 KB of LDS");
 __global__ void __launch_bounds__(256) ta_fine_partial(const float *__restrict__ ref, const float *__restrict__ deg,
                                                        int64_t B, int64_t L, int64_t ld,
                                                        const int32_t *__restrict__ lengths,
@@ -361,7 +366,9 @@ extern "C" int fsem_time_align_f32(const float *ref, const float *deg, int64_t b
   int *dl = delay ? delay : w.delay;
   const int64_t nfr_cap = std::max<int64_t>(align::frames_cap(length), 1);
   const int64_t sig = 2 * batch;
-  const int max_frames = (int)std::min<int64_t>((max_delay + align::FRAME - 1) / align::FRAME, INT32_MAX);
+  // 64-bit: max_delay may be INT32_MAX (alignment.py clamps to it), where the 32-bit sum would wrap
+  const int max_frames =
+      (int)std::min<int64_t>(((int64_t)max_delay + align::FRAME - 1) / align::FRAME, (int64_t)INT32_MAX);
   auto yz = [](int64_t n) { return dim3(1, (unsigned)std::min<int64_t>(n, 65535), (unsigned)((n + 65534) / 65535)); };
   {
     dim3 grid = yz(sig);

@@ -1422,12 +1422,53 @@ __global__ void __launch_bounds__(64 * BW) __attribute__((amdgpu_waves_per_eu(4)
   }
 }
 
+// Stage entry (fsem_pre_emphasize_f32): the pre-emphasis IIR of PESQ.pre_emphasize (PESQ.py:111)
+// as torchaudio's lfilter evaluates it -- FIR part over the zero-padded input (taps oldest
+// first), then the sequential all-pole loop acc = w - y[n-2] a2 - y[n-1] a1 -- with the
+// roundings written out (no contraction), so each output is the torchaudio-order float32 value.
+// One thread per row: a stage method off the scoring path (the scoring front end runs the same
+// filter time-parallel, pesq_front pass 2).
+__global__ void __launch_bounds__(64) pesq_pre_emphasis(const float *__restrict__ x, int64_t rows, int64_t L,
+                                                        int64_t ld, float *__restrict__ y, int64_t ld_out) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= rows) return;
+  const float *__restrict__ xr = x + r * ld;
+  float *__restrict__ yr = y + r * ld_out;
+  const float b0 = kPreB[2], b1 = kPreB[1], b2 = kPreB[0];  // flipped taps: x[n-2], x[n-1], x[n]
+  const float a2 = kPreA[2] / kPreA[0], a1 = kPreA[1] / kPreA[0];
+  float x1 = 0.f, x2 = 0.f, y1 = 0.f, y2 = 0.f;
+  for (int64_t n = 0; n < L; ++n) {
+    const float x0 = xr[n];
+    float w = __fmul_rn(b0, x2);
+    w = __fadd_rn(w, __fmul_rn(b1, x1));
+    w = __fadd_rn(w, __fmul_rn(b2, x0));
+    w = __fdiv_rn(w, kPreA[0]);
+    float acc = __fsub_rn(w, __fmul_rn(y2, a2));
+    acc = __fsub_rn(acc, __fmul_rn(y1, a1));
+    acc = __fsub_rn(acc, 0.f * 1.f);  // the loop's last term: the unwritten (zero) slot x a_flip[2] = 1
+    yr[n] = acc;
+    x2 = x1;
+    x1 = x0;
+    y2 = y1;
+    y1 = acc;
+  }
+}
+
 }  // namespace pesq
 }  // namespace fsem
 
 using namespace fsem;
 
 extern "C" int fsem_pesq_frames(int64_t length) { return pesq::frames_of(length); }
+
+extern "C" int fsem_pre_emphasize_f32(const float *x, int64_t rows, int64_t length, int64_t ld, float *y,
+                                      int64_t ld_out, void *stream) {
+  if (!x || !y || rows <= 0 || length <= 0 || ld < length || ld_out < length || length > kMaxLength) return FSEM_EINVAL;
+  hipLaunchKernelGGL(pesq::pesq_pre_emphasis, dim3((unsigned)((rows + 63) / 64)), dim3(64), 0, (hipStream_t)stream, x,
+                     rows, length, ld, y, ld_out);
+  FSEM_CHECK_LAUNCH();
+  return FSEM_OK;
+}
 
 #ifdef FSEM_STAMPS
 // diagnostic build only (not part of include/fsem.h)

@@ -9,8 +9,10 @@
  *
  * Host-side runtime code (no GPU): the Python equivalent, a dict display per row over
  * tensor.tolist(), costs about 80 ns per row on the MI355X box's host (profiles/r3_a/dropin.json,
- * 0.33 ms of an 8.6 ms call at B = 4096); this builds each dict presized and with the key
- * hashes cached, and never materialises the K intermediate lists.
+ * 0.33 ms of an 8.6 ms call at B = 4096); this builds each dict with the key hashes cached and
+ * never materialises the K intermediate lists.  Optional: where it cannot be built or loaded
+ * (no C compiler or Python headers, a read-only package directory), _native.score_list falls
+ * back to the Python form with the same result.
  */
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
@@ -48,7 +50,7 @@ static PyObject *score_list(PyObject *self, PyObject *args) {
   out = PyList_New(B);
   if (!out) goto done;
   for (Py_ssize_t b = 0; b < B; ++b) {
-    PyObject *d = _PyDict_NewPresized(K);
+    PyObject *d = PyDict_New(); /* public API; K <= 3 keys fit the minimum table */
     if (!d) goto fail;
     PyList_SET_ITEM(out, b, d); /* owned by the list from here (freed with it on failure) */
     for (Py_ssize_t k = 0; k < K; ++k) {

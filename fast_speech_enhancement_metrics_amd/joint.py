@@ -18,7 +18,7 @@ import torch
 from . import _native
 from .PESQ import PESQ
 from .STOI import STOI
-from .base import BaseMetric, as_rows, check_row_rate, device_lengths
+from .base import BaseMetric, as_rows, check_row_rate, device_lengths, noisy_shape
 
 
 _KEYS = ("PESQ", "STOI", "ESTOI")
@@ -28,10 +28,10 @@ class PESQ_STOI(BaseMetric):
     higher_is_better = True
     EXPECTED_SAMPLING_RATE = 16000
 
-    def __init__(self, sample_rate: int = 16000, use_gpu: bool = False):
-        super().__init__(sample_rate, use_gpu)
-        self._pesq = PESQ(sample_rate, use_gpu)
-        self._stoi = STOI(sample_rate, use_gpu)
+    def __init__(self, sample_rate: int = 16000, use_gpu: bool = False, *, devices=None):
+        super().__init__(sample_rate, use_gpu, devices=devices)
+        self._pesq = PESQ(sample_rate, use_gpu, devices=devices)
+        self._stoi = STOI(sample_rate, use_gpu, devices=devices)
 
     def __call__(self, clean_speech, denoised_speech, lengths=None) -> list[dict[str, float]]:
         if self.sample_rate == self.EXPECTED_SAMPLING_RATE:
@@ -59,6 +59,14 @@ class PESQ_STOI(BaseMetric):
             mos = self._pesq.scores(clean_speech, denoised_speech, lengths, sample_rate=sr)
             s, e = self._stoi.scores(clean_speech, denoised_speech, sr, lengths=lengths)
             return mos, s, e
+        if self.fans_out():
+            if noisy_shape(clean_speech) != noisy_shape(denoised_speech):
+                raise Exception("`clean_speech` and `denoised_speech` should have the same shape.")
+            return self.fan_out(self._rows_scores, clean_speech, denoised_speech, lengths, 3, balance=lengths)
+        return self._rows_scores(clean_speech, denoised_speech, lengths)
+
+    def _rows_scores(self, clean_speech, denoised_speech, lengths):
+        """(mos, stoi, estoi) [B] of 16 kHz rows on their own device (one fused engine call)."""
         clean = as_rows(clean_speech)
         noisy = as_rows(denoised_speech)
         if noisy.shape != clean.shape:
@@ -144,7 +152,8 @@ class PESQ_STOI(BaseMetric):
         """Row ranges of the engine calls the drop-in call makes for `batch` rows: one range, or
         batch // pipeline_rows consecutive ones on the GPU (bench.py times the dominant kernel and
         the scores path at this per-call size, so every launch in the bench has one size)."""
-        K = batch // self.pipeline_rows if (on_gpu and self.pipeline_rows > 0) else 1
+        # a multi-device call scores its shards concurrently already: one range
+        K = batch // self.pipeline_rows if (on_gpu and self.pipeline_rows > 0 and self._fanout is None) else 1
         K = max(K, 1)
         return [(k * batch // K, (k + 1) * batch // K) for k in range(K)]
 

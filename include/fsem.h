@@ -139,6 +139,14 @@ int fsem_pesq_back_f32(const float *bark, const float *power, int64_t batch, int
  *                 symmetric / asymmetric disturbances after the frame weighting and the clamp at
  *                 45 (PESQ.py:222-224); row b fills its first fsem_pesq_frames(lengths[b]) frames
  */
+/* pre-emphasis: replaces the lfilter of PESQ.pre_emphasize (PESQ.py:111; the edge taper of
+ *        :108-109 is the caller's, applied in place as the reference does) on any [rows, length]
+ *        float32 rows: y = lfilter(x, a = (1, -1.9444777, 0.94597794), b = (2.740826,
+ *        -5.4816519, 2.740826)) in torchaudio's float32 evaluation order (FIR then the all-pole
+ *        loop).  y [rows, length] float32, row stride ld_out (y may equal x only if ld_out == ld).
+ */
+int fsem_pre_emphasize_f32(const float *x, int64_t rows, int64_t length, int64_t ld, float *y,
+                           int64_t ld_out, void *stream);
 size_t fsem_pesq_distances_workspace_bytes(int64_t batch, int64_t length);
 int fsem_pesq_distances_f32(const float *bark, const float *power, int64_t batch, int64_t length,
                             const int32_t *lengths, float *dist, float *frames, void *ws,

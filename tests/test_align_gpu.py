@@ -61,6 +61,19 @@ def test_engine_edge_rows(dev):
     assert ds.tolist() == [A.delay(r, r) for r in x.cpu().numpy()] == [0, 0]
 
 
+def test_engine_unbounded_max_delay(dev):
+    """max_delay = 2**31 - 1 (the C-ABI's int32 maximum, alignment.py's clamp): the crude search
+    covers every lag, as the CPU path and the oracle do (its frame count used to wrap in 32 bits,
+    which turned the crude search off on the GPU)."""
+    from fast_speech_enhancement_metrics_amd.alignment import time_align
+    c, deg, D = _delayed(6, 48000, 36, 3000)
+    big = 2**31 - 1
+    _, ds = time_align(torch.from_numpy(c).to(dev), torch.from_numpy(deg).to(dev), max_delay=big)
+    _, dcpu = time_align(torch.from_numpy(c), torch.from_numpy(deg), max_delay=big)
+    np.testing.assert_array_equal(ds.cpu().numpy(), dcpu.numpy())
+    np.testing.assert_array_equal(ds.cpu().numpy(), D)
+
+
 def test_pesq_time_align_on_gpu(dev):
     from fast_speech_enhancement_metrics_amd import PESQ
     c, deg, D = _delayed(12, 48000, 33, 3000)

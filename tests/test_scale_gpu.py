@@ -74,3 +74,26 @@ def test_dropin_call_equals_scores_at_bench_size(batch):
     np.testing.assert_array_equal(np.array([d["PESQ"] for d in res], dtype=np.float32), mos)
     np.testing.assert_array_equal(np.array([d["STOI"] for d in res], dtype=np.float32), s)
     np.testing.assert_array_equal(np.array([d["ESTOI"] for d in res], dtype=np.float32), e)
+
+
+def test_pesq_only_entry_at_bench_size(batch):
+    """BASELINE.json configs[1] as stated (PESQ-wb alone, 4096 x 10 s): PESQ(16000).scores runs the
+    PESQ-only front-end instance (fsem_pesq_wb_f32 -> pesq_front<false, false, false>), whose row
+    offsets pass 2^31 bytes from row 3277 on.  Sampled rows agree with the oracle; the MOS equals
+    the joint entry's on the same batch bitwise; two runs are bitwise identical; the drop-in call
+    returns the same values."""
+    from fast_speech_enhancement_metrics_amd import PESQ, PESQ_STOI
+    c, n = batch
+    m = PESQ(16000, use_gpu=True)
+    mos = m.scores(c, n).cpu().numpy()
+    np.testing.assert_array_equal(m.scores(c, n).cpu().numpy(), mos)
+    assert np.isfinite(mos).all() and (mos >= 1.0).all() and (mos <= 4.65).all()
+    joint = PESQ_STOI(16000, use_gpu=True).scores(c, n)[0].cpu().numpy()
+    np.testing.assert_array_equal(mos, joint)
+    cc, nn = c[ROWS].cpu().numpy(), n[ROWS].cpu().numpy()
+    op = pesq_oracle.pesq(cc, nn)
+    dp = np.abs(mos[ROWS] - op).max()
+    print(f"PESQ-only entry, rows {ROWS}: max |dPESQ| {dp:.2e} vs oracle")
+    assert dp < PESQ_TOL
+    res = m(c, n)
+    np.testing.assert_array_equal(np.array([d["PESQ"] for d in res], dtype=np.float32), mos)

@@ -46,3 +46,64 @@ def test_rejects_bad_input():
         _native.score_list(np.zeros((1, 4), np.float32), ())
     with pytest.raises(TypeError):
         _native.score_list(np.zeros((1, 4), np.float32), (1,))
+
+
+@pytest.fixture
+def python_builder(monkeypatch):
+    """The native builder unavailable (as without a C compiler / Python headers / a writable
+    package directory): _native.score_list takes the Python form."""
+    monkeypatch.setattr(_native, "_score_list_mod", False)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+def test_python_fallback_matches_native(dtype, python_builder):
+    g = torch.Generator().manual_seed(1)
+    t = torch.randn(3, 257, generator=g, dtype=dtype)
+    t[2, 5] = float("nan")
+    keys = ("PESQ", "STOI", "ESTOI")
+    got = _native.score_list(t, keys)
+    want = _py(t, keys)
+    assert len(got) == len(want)
+    for a, b in zip(got, want):
+        assert list(a) == list(keys)
+        for k in keys:
+            assert (math.isnan(a[k]) and math.isnan(b[k])) or a[k] == b[k]
+            assert type(a[k]) is float
+
+
+def test_python_fallback_checks(python_builder):
+    assert _native.score_list(torch.tensor([[1.5, 2.0]]), ("PESQ",)) == [{"PESQ": 1.5}, {"PESQ": 2.0}]
+    assert _native.score_list(np.zeros((2, 0), np.float32), ("STOI", "ESTOI")) == []
+    with pytest.raises(TypeError):
+        _native.score_list(np.zeros((3, 4), np.int32), ("a", "b", "c"))
+    with pytest.raises(TypeError):
+        _native.score_list(np.zeros(5, np.float32), ("a", "b", "c"))
+    with pytest.raises(ValueError):
+        _native.score_list(np.zeros((1, 4), np.float32), ())
+    with pytest.raises(TypeError):
+        _native.score_list(np.zeros((1, 4), np.float32), (1,))
+
+
+def test_drop_in_call_without_native_builder(python_builder):
+    """The CPU-mode drop-in call works (same list) when the native builder cannot be built."""
+    from fast_speech_enhancement_metrics_amd import STOI
+    from fast_speech_enhancement_metrics_amd.synthetic import speech_like_pairs
+    c, n, _ = speech_like_pairs(2, 16000, 10000, seed=3)
+    s, e = STOI(10000).scores(c, n)
+    got = STOI(10000)(c, n)
+    assert got == [{"STOI": float(a), "ESTOI": float(b)} for a, b in zip(s.float().tolist(), e.float().tolist())]
+
+
+def test_unbuildable_native_builder_falls_back(monkeypatch):
+    """A failing build (e.g. no C compiler) warns once and leaves the Python form in place."""
+    from fast_speech_enhancement_metrics_amd import _build
+
+    def broken(*a, **k):
+        raise RuntimeError("no C compiler found")
+
+    monkeypatch.setattr(_native, "_score_list_mod", None)
+    monkeypatch.setattr(_build, "build_score_list", broken)
+    with pytest.warns(RuntimeWarning, match="native score-list builder unavailable"):
+        got = _native.score_list(np.array([[1.0, 2.0]], np.float32), ("PESQ",))
+    assert got == [{"PESQ": 1.0}, {"PESQ": 2.0}]
+    assert _native._score_list_mod is False

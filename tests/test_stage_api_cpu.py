@@ -111,6 +111,9 @@ def test_pesq_stages_match_reference(name):
     np.testing.assert_allclose(scale.numpy(), g["level_scale"], rtol=3e-3)
     # pre-emphasis: taper in place, then the IIR -- spectrum + filterbank of it give the bands
     pre = m.pre_emphasize(aligned.clone())
+    # the reference's stage dtypes: align_level / pre_emphasize float32 (lfilter keeps the input's),
+    # get_bark_bands float64 (bark.py:204's float64 correction)
+    assert aligned.dtype == torch.float32 and pre.dtype == torch.float32
     spec = m.to_spec(torch.nn.functional.pad(pre, (0, pre.shape[1] % 256))).swapaxes(1, 2)
     spec[:, :, 0] = 0.0
     bark2 = m.filter_bank(spec.double())

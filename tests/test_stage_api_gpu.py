@@ -99,3 +99,33 @@ def test_stoi_stage_methods_on_gpu(dev):
     s, e = m.compute_stoi(c, n)
     np.testing.assert_allclose(s.cpu().numpy(), g["stoi"], atol=5e-4, rtol=0)
     np.testing.assert_allclose(e.cpu().numpy(), g["estoi"], atol=5e-4, rtol=0)
+
+
+def test_stage_dtypes_and_devices_match_reference(dev):
+    """The reference's stage outputs (PESQ.py:92-140): align_level and pre_emphasize float32 (its
+    lfilter keeps the input dtype), get_bark_bands float64 (BarkFilterBank.forward multiplies by
+    the float64 pow_dens_correction, bark.py:132,204); every one on the input's device -- on a
+    use_gpu=True metric pre_emphasize never leaves the device.  Rows shorter than one 512-sample
+    frame still level-align (the reference filters any length)."""
+    from fast_se_metrics import PESQ
+    from oracle import ta
+    m = PESQ(16000, use_gpu=True)
+    g = load_golden("pesq_3s")
+    x = torch.from_numpy(g["clean_f"]).to(dev)
+    al = m.align_level(x.clone())
+    assert al.dtype == torch.float32 and al.is_cuda
+    pe_in = al.clone()
+    pe = m.pre_emphasize(pe_in)
+    assert pe.dtype == torch.float32 and pe.is_cuda
+    # bitwise the torchaudio-order float32 lfilter (oracle/c/lfilter_f32.c) of the tapered rows
+    # (pre_emphasize tapers its argument in place, as the reference)
+    want = ta.lfilter(pe_in.cpu().numpy(), np.array([1.0, -1.9444777, 0.94597794], np.float32),
+                      np.array([2.740826, -5.4816519, 2.740826], np.float32))
+    np.testing.assert_array_equal(pe.cpu().numpy(), want)
+    bark = m.get_bark_bands(x.clone())
+    assert bark.dtype == torch.float64 and bark.is_cuda
+    short = torch.randn(3, 300, device=dev)
+    s_al = m.align_level(short)
+    assert s_al.dtype == torch.float32 and s_al.is_cuda and torch.isfinite(s_al).all()
+    cpu = PESQ(16000).align_level(short.cpu())
+    np.testing.assert_allclose(s_al.cpu().numpy(), cpu.numpy(), rtol=1e-6, atol=0)
