@@ -1430,6 +1430,7 @@ __global__ void __launch_bounds__(64 * BW) __attribute__((amdgpu_waves_per_eu(4)
 // filter time-parallel, pesq_front pass 2).
 __global__ void __launch_bounds__(64) pesq_pre_emphasis(const float *__restrict__ x, int64_t rows, int64_t L,
                                                         int64_t ld, float *__restrict__ y, int64_t ld_out) {
+#pragma clang fp contract(off)  // every product rounded on its own, as the C loop
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= rows) return;
   const float *__restrict__ xr = x + r * ld;
@@ -1439,13 +1440,12 @@ __global__ void __launch_bounds__(64) pesq_pre_emphasis(const float *__restrict_
   float x1 = 0.f, x2 = 0.f, y1 = 0.f, y2 = 0.f;
   for (int64_t n = 0; n < L; ++n) {
     const float x0 = xr[n];
-    float w = __fmul_rn(b0, x2);
-    w = __fadd_rn(w, __fmul_rn(b1, x1));
-    w = __fadd_rn(w, __fmul_rn(b2, x0));
-    w = __fdiv_rn(w, kPreA[0]);
-    float acc = __fsub_rn(w, __fmul_rn(y2, a2));
-    acc = __fsub_rn(acc, __fmul_rn(y1, a1));
-    acc = __fsub_rn(acc, 0.f * 1.f);  // the loop's last term: the unwritten (zero) slot x a_flip[2] = 1
+    float w = b0 * x2;
+    w = w + b1 * x1;
+    w = w + b2 * x0;
+    w = w / kPreA[0];
+    float acc = w - y2 * a2;
+    acc = acc - y1 * a1;  // (the loop's last term, the unwritten zero slot x a_flip[2] = 1, adds -0)
     yr[n] = acc;
     x2 = x1;
     x1 = x0;

@@ -12,9 +12,9 @@
 //  stoi_select   per utterance: frame energies in dB, 40 dB voice-activity selection against the
 //                loudest clean frame, stream compaction of the kept frame indices (STOI.py:101-108).
 //  stoi_tob      per (utterance, 32 STFT frames): overlap-added signal built directly from
-//                the kept frames (STOI.py:71-86, never materialised), 512-point FFT of
-//                clean + i*denoised (one wave per frame pair), 15 one-third-octave band
-//                envelopes (STOI.py:49-69, 121-125).
+//                the kept frames (STOI.py:71-86, never materialised), 512-point FFTs of two
+//                consecutive frames of one signal (one wave per frame pair), 15 one-third-octave
+//                band envelopes (STOI.py:49-69, 121-125).
 //  stoi_seg      per utterance: 30-frame segments -- equalisation + clipping, row / column
 //                normalisation and correlations for STOI and ESTOI (STOI.py:113-198), one
 //                lane per segment, band envelopes staged in LDS (no 30x materialisation).
@@ -408,45 +408,57 @@ __global__ void __launch_bounds__(64 * TOB_WAVES)
   const int pc_lo = kObmPiece[lane][2], pc_hi = kObmPiece[lane][3];
   const int pc_end = kObmPiece[lane][4];
   const bool pc_head = kObmPiece[lane][5] != 0;
-  for (int k = k0 + wave; k < kend; k += TOB_WAVES) {
-    const int j = k - k0;  // frame k = [block_{k+1}, block_{k+2}] * w
+  // Two consecutive STFT frames of ONE signal per complex FFT (z = frame a + i frame b): the
+  // Hermitian split recovers each from Z[k] -/+ conj(Z[N-k]), whose rounding is relative to |Z|
+  // in that bin, i.e. to the two frames' own spectra there.  (Pairing clean with denoised instead
+  // let a loud clean band leak into a denoised band 100 dB below it -- tone-probe rows whose
+  // denoised signal is a pure tone got 2-3x the float32 noise floor of a separate transform in
+  // their off-tone bands, tools/tob_dump.py.)  Neighbouring frames share half their samples, so
+  // their spectra are alike except at onsets, which the peak equalisation below covers.
+  const int nfr = kend - k0;
+  const int nfft = 2 * ((nfr + 1) >> 1);  // (signal, frame pair) transforms of this workgroup
+  for (int f = wave; f < nfft; f += TOB_WAVES) {
+    const int sg = f & 1;          // signal (wave-uniform: TOB_WAVES is even)
+    const int ja = 2 * (f >> 1);   // frame a = k0 + ja = [block_{ja}, block_{ja+1}] * w, frame b = a + 1
+    const bool has_b = ja + 1 < nfr;
     cf v[8];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int jj = j + (r >> 1), t = lane + 64 * (r & 1);
-      v[r] = {blk[0][jj][t] * win[r], blk[1][jj][t] * win[r]};
+      const int t = lane + 64 * (r & 1);
+      const float a = blk[sg][ja + (r >> 1)][t];
+      const float bq = has_b ? blk[sg][ja + 1 + (r >> 1)][t] : 0.f;  // (uniform)
+      v[r] = {a * win[r], bq * win[r]};
     }
 #pragma unroll
     for (int r = 4; r < 8; ++r) v[r] = {0.f, 0.f};
-    // An all-zero frame of one signal has an exactly zero spectrum, but the shared complex FFT's
-    // rounding is not exactly Hermitian: ~1e-7 of the other signal's spectrum would leak into
-    // it, and the segment normalisation (STOI.py:113-119) would turn that leak into a
-    // correlation (an all-zero denoised signal would score ~0.8 instead of 0).
-    // The same rounding leaks ~1e-7 of the louder signal's spectrum into the quieter one's
-    // whatever their levels, so a frame whose denoised signal sits ~100 dB or more below the clean
-    // one (e.g. int16-scaled clean against float denoised) would lose its spectrum to the leak.
-    // Frames with a gap of 2^7 or more in peak sample are equalised first: the denoised half is
-    // scaled by 2^sh to the clean half's peak exponent (exact in floating point), its power by
-    // 2^-2sh after the FFT (exact again).
+    // An all-zero frame has an exactly zero spectrum, but the shared transform's rounding is not
+    // exactly Hermitian: ~1e-7 of the other frame's spectrum would leak into it, and the segment
+    // normalisation (STOI.py:113-119) would turn that leak into a correlation (an all-zero
+    // denoised signal next to non-zero frames would score like noise, not 0).
+    // The same rounding leaks ~1e-7 of the louder frame's spectrum into the quieter one's, so a
+    // frame ~100 dB or more below its neighbour (an onset after silence) would lose its spectrum
+    // to the leak.  Pairs with a gap of 2^7 or more in peak sample are equalised first: frame b
+    // is scaled by 2^sh to frame a's peak exponent (exact in floating point), its power by 2^-2sh
+    // after the FFT (exact again).
     const uint32_t pk = peak_exponents(v[0].r, v[1].r, v[2].r, v[3].r, v[0].i, v[1].i, v[2].i, v[3].i);
-    const int ec = (int)(pk >> 16), ed = (int)(pk & 0xffffu);
-    const bool c_zero = ec == 0 && !__any(v[0].r != 0.f || v[1].r != 0.f || v[2].r != 0.f || v[3].r != 0.f);
-    const bool d_zero = ed == 0 && !__any(v[0].i != 0.f || v[1].i != 0.f || v[2].i != 0.f || v[3].i != 0.f);
-    int sh = (ec > 0 && ed > 0) ? ec - ed : 0;
+    const int ea = (int)(pk >> 16), eb = (int)(pk & 0xffffu);
+    const bool a_zero = ea == 0 && !__any(v[0].r != 0.f || v[1].r != 0.f || v[2].r != 0.f || v[3].r != 0.f);
+    const bool b_zero = eb == 0 && !__any(v[0].i != 0.f || v[1].i != 0.f || v[2].i != 0.f || v[3].i != 0.f);
+    int sh = (ea > 0 && eb > 0) ? ea - eb : 0;
     sh = (sh >= 7 || sh <= -7) ? max(-60, min(60, sh)) : 0;
     if (sh != 0) {  // uniform
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r].i = __builtin_amdgcn_ldexpf(v[r].i, sh);
     }
     // wave-uniform factors, applied to the band envelopes after the square root (powers of two:
-    // the same values as scaling every bin's power by 0.25 (x 2^-2sh for the denoised power),
+    // the same values as scaling every bin's power by 0.25 (x 2^-2sh for frame b's power),
     // short of under/overflow), or 0 for a zero frame.  Scaling after the root keeps the
     // hardware sqrt's input at the equalised level: v_sqrt_f32 loses accuracy on tiny and
-    // denormal inputs, which a quiet denoised frame scaled down first would feed it.
-    const float c_scale = c_zero ? 0.f : 0.5f;
-    const float d_scale = d_zero ? 0.f : __builtin_amdgcn_ldexpf(0.5f, -sh);
+    // denormal inputs, which a quiet frame scaled down first would feed it.
+    const float a_scale = a_zero ? 0.f : 0.5f;
+    const float b_scale = b_zero ? 0.f : __builtin_amdgcn_ldexpf(0.5f, -sh);
     fft512_wave<true>(v, wbuf, lane, tw1, tw2);  // v[4..7] = 0: the frame's zero-padded half
-    float pc[4], pd[4];
+    float pa[4], pb[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       float mr = __shfl(v[7 - r].r, plane, 64);
@@ -456,21 +468,22 @@ __global__ void __launch_bounds__(64 * TOB_WAVES)
         mi = v[(8 - r) & 7].i;
       }
       const float zr = v[r].r, zi = v[r].i;
-      pc[r] = fmaf(zr + mr, zr + mr, (zi - mi) * (zi - mi));  // explicit: no contraction choice
-      pd[r] = fmaf(zi + mi, zi + mi, (zr - mr) * (zr - mr));
+      pa[r] = fmaf(zr + mr, zr + mr, (zi - mi) * (zi - mi));  // explicit: no contraction choice
+      pb[r] = fmaf(zi + mi, zi + mi, (zr - mr) * (zr - mr));
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      lds_store_lanes(pbuf + 64 * r, pc[r]);
-      lds_store_lanes(pbuf + 256 + 64 * r, pd[r]);
+      lds_store_lanes(pbuf + 64 * r, pa[r]);
+      lds_store_lanes(pbuf + 256 + 64 * r, pb[r]);
     }
     wave_lds_fence();
     {
-      // band sums: one <=9-bin piece per lane, segmented shuffle reduction per band
+      // band sums: one <=9-bin piece per lane (lanes of piece set 0: frame a, set 1: frame b),
+      // segmented shuffle reduction per band
       const float *ps = pbuf + 256 * pc_sig;
       float acc = 0.f;
 #pragma unroll
-      for (int i = 0; i < 9; ++i) {  // unconditional reads (inside the signal's 256 powers), masked adds
+      for (int i = 0; i < 9; ++i) {  // unconditional reads (inside the frame's 256 powers), masked adds
         const float x = ps[pc_lo + i];
         acc += (pc_lo + i < pc_hi) ? x : 0.f;
       }
@@ -481,8 +494,9 @@ __global__ void __launch_bounds__(64 * TOB_WAVES)
       }
       // hardware square root (1 ulp; the correctly rounded sqrtf is a ~17-instruction sequence
       // that every lane of the wave issues)
-      if (pc_head)
-        tob[((b + pc_sig * B) * NB + pc_band) * tmax + k] = __builtin_amdgcn_sqrtf(acc) * (pc_sig ? d_scale : c_scale);
+      if (pc_head && (pc_sig == 0 || has_b))
+        tob[((b + sg * B) * NB + pc_band) * tmax + k0 + ja + pc_sig] =
+            __builtin_amdgcn_sqrtf(acc) * (pc_sig ? b_scale : a_scale);
     }
     wave_lds_fence();
   }
@@ -589,7 +603,11 @@ __global__ void __launch_bounds__(SEG_T, 3)
         const float rxn = __builtin_amdgcn_rsqf(dd.x + kReg30);
         const float ryn = __builtin_amdgcn_rsqf(dd.y + kReg30);
         const float rcn = __builtin_amdgcn_rsqf(dcc + kReg30);
-        s_acc = fmaf(dxc * rxn, rcn, s_acc);
+        // torch.minimum (STOI.py:139) propagates a NaN of the scaled denoised row, fminf drops
+        // it: a NaN / Inf denoised row (alpha non-finite) poisons the sum as in the reference.
+        // (A select, not alpha - alpha: contracted into fma(a, b, -(a b)) that difference is the
+        // product's rounding error, not 0.)
+        s_acc = fmaf(dxc * rxn, rcn, s_acc) + (__builtin_isfinite(alpha) ? 0.f : __builtin_nanf(""));
         rxy[j] = (f2){rxn, ryn};
         nvar = __builtin_elementwise_fma(rxy[j], rxy[j], nvar);
         nmr[j] = -mu * rxy[j];

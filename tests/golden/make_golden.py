@@ -190,6 +190,50 @@ def _reference_stoi(clean, noisy, sr: int, seed: int):
     return np.array([r["STOI"] for r in res]), np.array([r["ESTOI"] for r in res])
 
 
+# Per-row alternate evaluations of the reference: the same scores evaluated
+# again in float32 -- STOI / ESTOI with torch seed 1 (its 1e-12 * randn, STOI.py:116) and on the
+# input scaled by non-dyadic factors (STOI is scale-invariant, so each is another float32
+# evaluation of the same scores; a power of two would give bitwise the same floats), PESQ with
+# the shim's float64-accumulated FIR order and on the scaled input (the level alignment,
+# PESQ.py:92-102, removes any common scale) -- plus the oracle's float64 evaluation of the
+# reference's math on the very same float32 input (oracle/*_oracle.py, pinned to the reference
+# by tests/test_oracle_golden.py), i.e. where exact arithmetic puts the score.  Stored per row
+# as <key>_alts [n_alt, B] with the row names in alt_names_<metric>.
+ALT_SCALES = (0.75, 0.6, 0.9, 1.1, 1.3)
+
+
+def _oracle_scores(clean, noisy, sr: int, metric: str):
+    sys.path.insert(0, REPO)
+    from oracle import pesq_oracle, stoi_oracle
+    c, n = clean.numpy(), noisy.numpy()
+    if metric == "pesq":
+        return pesq_oracle.pesq(c, n)
+    return stoi_oracle.stoi(c, n, sr)
+
+
+def stoi_alts(clean, noisy, sr: int):
+    """(names, stoi_alts [n, B], estoi_alts [n, B]) of the reference's re-evaluations + float64."""
+    names, S, E = [], [], []
+    s, e = _reference_stoi(clean, noisy, sr, 1)
+    names.append("seed1"); S.append(s); E.append(e)
+    for m in ALT_SCALES:
+        s, e = _reference_stoi(clean * m, noisy * m, sr, 0)
+        names.append(f"x{m}"); S.append(s); E.append(e)
+    s, e = _oracle_scores(clean, noisy, sr, "stoi")
+    names.append("float64"); S.append(s); E.append(e)
+    return np.array(names), np.stack(S), np.stack(E)
+
+
+def pesq_alts(clean, noisy):
+    names, P = ["fir_f64"], [_reference_pesq(clean, noisy, "f64")]
+    for m in ALT_SCALES:
+        names.append(f"x{m}")
+        P.append(_reference_pesq(clean * m, noisy * m))
+    names.append("float64")
+    P.append(_oracle_scores(clean, noisy, 16000, "pesq"))
+    return np.array(names), np.stack(P)
+
+
 # Edge inputs (VERDICT r2 item 1): a speech-like int16-grid pair transformed in float32 by
 #   x = codes / 32768 * scale + offset
 # (torch float32 ops, so the GPU tests rebuild the exact inputs from the stored codes).  The
@@ -230,6 +274,8 @@ def edge_case(name: str = "edges_16k"):
         # 0.75 x the same pair is another float32 evaluation of the same scores
         s75, e75 = _reference_stoi(c * 0.75, n * 0.75, 16000, 0)
         out[k + "_stoi_x075"], out[k + "_estoi_x075"] = s75, e75
+        out["alt_names_stoi"], out[k + "_stoi_alts"], out[k + "_estoi_alts"] = stoi_alts(c, n, 16000)
+        out["alt_names_pesq"], out[k + "_pesq_alts"] = pesq_alts(c, n)
         print(k, out[k + "_pesq"], out[k + "_pesq_f64fir"], out[k + "_stoi"], out[k + "_stoi_seed1"],
               out[k + "_estoi"], out[k + "_estoi_seed1"], "x0.75:", s75 - out[k + "_stoi"], e75 - out[k + "_estoi"])
     print("base", out["base_pesq"], out["base_stoi"], out["base_estoi"])
@@ -255,12 +301,36 @@ def tone_probe_case(name: str = "tone_probe_10k"):
     out["stoi"], out["estoi"] = _reference_stoi(ct, dt, 10000, 0)
     out["stoi_seed1"], out["estoi_seed1"] = _reference_stoi(ct, dt, 10000, 1)
     out["stoi_x075"], out["estoi_x075"] = _reference_stoi(ct * 0.75, dt * 0.75, 10000, 0)
+    out["alt_names_stoi"], out["stoi_alts"], out["estoi_alts"] = stoi_alts(ct, dt, 10000)
     np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
     print(name, out["stoi"], out["estoi"], out["stoi_seed1"] - out["stoi"], out["estoi_seed1"] - out["estoi"],
           out["stoi_x075"] - out["stoi"], out["estoi_x075"] - out["estoi"])
 
 
+def lowpass_case(name: str = "lowpass_10k"):
+    """Denoised = the clean signal through a float64 elliptic low-pass, rounded to float32
+    (VERDICT r3 item 1): the sample peaks of the two stay within a factor ~2-5 while the upper
+    third-octave bands of the denoised signal sit 80-100 dB below the clean's -- the case where a
+    clean/denoised cross-talk in a shared FFT would show.  STOI(10000) with the per-row alternates."""
+    from scipy.signal import ellip, sosfilt
+    clean, _, _ = speech_like_pairs(4, 30000, 10000, seed=21)
+    c = clean.numpy().astype(np.float32)
+    rows = []
+    for r, (fc, att) in enumerate(((1000, 120), (800, 140), (1500, 160), (1000, 120))):
+        sos = ellip(10, 0.1, att, fc, fs=10000, output="sos")
+        rows.append(sosfilt(sos, c[r].astype(np.float64)).astype(np.float32))
+    d = np.stack(rows)
+    out = dict(clean_f32=c, noisy_f32=d, sample_rate=10000)
+    ct, dt = torch.from_numpy(c), torch.from_numpy(d)
+    out["stoi"], out["estoi"] = _reference_stoi(ct, dt, 10000, 0)
+    out["alt_names_stoi"], out["stoi_alts"], out["estoi_alts"] = stoi_alts(ct, dt, 10000)
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
+    print(name, out["stoi"], out["estoi"], np.abs(out["stoi_alts"] - out["stoi"]).max(0),
+          np.abs(out["estoi_alts"] - out["estoi"]).max(0))
+
+
 CASES = {
+    "lowpass_10k": lowpass_case,
     "edges_16k": edge_case,
     "tone_probe_10k": tone_probe_case,
     "pesq_3s": lambda: pesq_case("pesq_3s", batch=4, length=48000, seed=1),

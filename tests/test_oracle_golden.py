@@ -72,3 +72,28 @@ def test_oracle_stoi_tones_within_reference_conditioning():
     s, e = stoi_oracle.stoi(g["clean_f"], g["noisy_f"], int(g["sample_rate"]))
     np.testing.assert_allclose(s, g["stoi"], atol=1e-3, rtol=0)
     np.testing.assert_allclose(e, g["estoi"], atol=1.5e-3, rtol=0)
+
+
+def test_oracle_stoi_lowpass_and_alternates_consistent():
+    """lowpass_10k (denoised = low-passed clean, upper bands 80-100 dB down): the oracle agrees with
+    the reference to its own re-evaluation spread, and the golden's last alternate row is this
+    oracle's float64 evaluation (make_golden.py stoi_alts)."""
+    g = load_golden("lowpass_10k")
+    s, e = stoi_oracle.stoi(g["clean_f"], g["noisy_f"], 10000)
+    assert list(g["alt_names_stoi"])[-1] == "float64"
+    np.testing.assert_allclose(s, g["stoi_alts"][-1], rtol=0, atol=1e-12)
+    np.testing.assert_allclose(e, g["estoi_alts"][-1], rtol=0, atol=1e-12)
+    np.testing.assert_allclose(s, g["stoi"], atol=1e-4, rtol=0)
+    np.testing.assert_allclose(e, g["estoi"], atol=2e-3, rtol=0)
+
+
+def test_edge_alternates_are_reference_reevaluations():
+    """edges_16k / tone_probe_10k carry >= 5 alternate evaluations per row (VERDICT r3 item 1);
+    the seed-1 row equals the stored seed-1 scores."""
+    for name in ("edges_16k", "tone_probe_10k"):
+        g = load_golden(name)
+        names = list(g["alt_names_stoi"])
+        assert len(names) >= 5 and names[0] == "seed1" and names[-1] == "float64"
+    e = load_golden("edges_16k")
+    np.testing.assert_array_equal(e["dc1000_both_stoi_alts"][0], e["dc1000_both_stoi_seed1"])
+    assert len(e["alt_names_pesq"]) >= 5
