@@ -17,7 +17,10 @@ Weak scaling: every rank owns its own shard of utterances, generated in HBM befo
 
 ``--gpus N`` without a torch.distributed launcher starts the N ranks itself (a child
 ``torch.distributed.run`` process, before this process touches the GPU); N above the visible
-device count is an error.
+device count is an error.  This one-process-per-GPU form is what the driver's scaling runs time.
+``--gpus N --single-process`` times the other multi-device form instead: one process driving N
+devices through ``PESQ_STOI(..., devices=N)`` (multidevice.py) on a batch held by device 0, the
+shards' peer copies included.
 
 Rank 0 prints ONE JSON line with the metric, the roofline of the dominant kernel
 (pesq_front<joint>: algorithmic bytes / its HIP-event-timed duration vs 8 TB/s), the CPU
@@ -56,6 +59,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=5)
     ap.add_argument("--separate", action="store_true", help="two API calls (PESQ, STOI) instead of the joint entry")
+    ap.add_argument("--single-process", action="store_true",
+                    help="with --gpus N: ONE process drives the N devices (devices=N on the metric, "
+                         "multidevice.py) on a batch of N x --batch rows held by device 0 -- the timed "
+                         "call includes the peer copies of the other devices' shards over xGMI")
     ap.add_argument("--workload", default="c2", choices=["c2", "pesq", "pesq_aligned", "c3", "c5"],
                     help="c2: BASELINE metric (default, PESQ-wb + STOI/ESTOI); pesq: configs[1] as stated, "
                          "PESQ-wb only; c3: STOI+ESTOI only, 8192 x 5 s @ 16 kHz per GPU; "
@@ -442,8 +449,50 @@ def spawn_ranks(n: int) -> int:
     return subprocess.call(cmd)
 
 
+def run_single_process(args):
+    """--single-process: the drop-in call PESQ_STOI(16000, use_gpu=True, devices=N)(clean, noisy)
+    from one process on N x --batch rows resident on device 0 (the reference user's batch on
+    "cuda"): each shard is copied to its device over xGMI inside the timed call, scored there on
+    its own stream, and the scores come back to device 0 (multidevice.py)."""
+    from fast_speech_enhancement_metrics_amd import PESQ_STOI
+    from fast_speech_enhancement_metrics_amd.synthetic import speech_like_pairs
+    n = args.gpus
+    visible = torch.cuda.device_count()
+    if n > visible:
+        print(f"bench.py: --gpus {n} but only {visible} HIP device(s) are visible", file=sys.stderr)
+        sys.exit(2)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    B, L = n * args.batch, args.length
+    cs, ns = [], []
+    for lo in range(0, B, 2048):
+        c, x, _ = speech_like_pairs(min(2048, B - lo), L, 16000, seed=42 + lo, device=dev)
+        cs.append(c)
+        ns.append(x)
+    clean, noisy = torch.cat(cs), torch.cat(ns)
+    del cs, ns
+    metric = PESQ_STOI(16000, use_gpu=True, devices=n)
+
+    def step():
+        return metric(clean, noisy)
+
+    dt = _timed(step, args, dev, False)
+    print(json.dumps({
+        "metric": METRIC + " (one process, devices=N)", "value": round(B * args.steps / dt, 2),
+        "unit": "utterances/s", "n_gpus": n, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic speech-like pairs, the whole batch on device 0",
+        "config": {"workload": "PESQ_STOI(16000, use_gpu=True, devices=N)(c, n) -> list of dicts, including the "
+                               "peer copies of N-1 shards from device 0", "batch_per_gpu": args.batch,
+                   "global_batch": B, "length": L, "sample_rate": 16000,
+                   "parallelism": f"{n} devices from one process (multidevice.py)"}}), flush=True)
+
+
 def main():
     args = parse()
+    if args.single_process:
+        run_single_process(args)
+        return
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))

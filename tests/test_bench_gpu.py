@@ -67,3 +67,17 @@ def test_bench_rccl_path_one_rank_pipelined():
     assert len(lines) == 1, out.stdout
     d = json.loads(lines[0])
     assert d["n_gpus"] == 1 and d["value"] > 0 and d["config"]["batch_per_gpu"] == 4096
+
+
+def test_bench_single_process_mode():
+    """--single-process: one process drives the devices through PESQ_STOI(devices=N) (here N = 1,
+    the 1-GPU box): one JSON line with the throughput of the whole batch."""
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "1", "--single-process",
+                          "--batch", "64", "--length", "48000", "--steps", "2", "--warmup", "1"],
+                         cwd=REPO, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, out.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 1 and d["config"]["global_batch"] == 64 and d["value"] > 0
+    assert "devices=N" in d["config"]["workload"]

@@ -39,6 +39,11 @@ def main(root: str):
             d["hbm_write_bytes"] = 1024 * d["WRITE_SIZE"]
         if "hbm_read_bytes" in d and "hbm_write_bytes" in d:
             d["hbm_bytes"] = d["hbm_read_bytes"] + d["hbm_write_bytes"]
+        if "SQ_WAVE_CYCLES" in d and d.get("GRBM_GUI_ACTIVE"):
+            # mean resident waves per SIMD over the launch: SQ_WAVE_CYCLES counts quad-cycles
+            # (x4), GRBM_GUI_ACTIVE is summed over the 8 XCDs (/8 = the launch's cycles), and
+            # the chip has 256 CUs x 4 SIMDs (tools/gpu_round.sh collects both in its SQ pass).
+            d["waves_per_simd"] = 4 * d["SQ_WAVE_CYCLES"] / (d["GRBM_GUI_ACTIVE"] / 8 * 1024)
         out[k] = d
     # the engine call the passes profiled (tools/one_step.py: the drop-in call's row chunk)
     out["_meta"] = {"rows_per_launch": int(os.environ.get("PMC_ROWS", "4096")),
