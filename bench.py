@@ -63,7 +63,8 @@ def parse():
                     help="with --gpus N: ONE process drives the N devices (devices=N on the metric, "
                          "multidevice.py) on a batch of N x --batch rows held by device 0 -- the timed "
                          "call includes the peer copies of the other devices' shards over xGMI")
-    ap.add_argument("--workload", default="c2", choices=["c2", "pesq", "pesq_aligned", "c3", "c5"],
+    ap.add_argument("--workload", default="c2",
+                    choices=["c2", "pesq", "pesq_aligned", "pesq_aligned_utt", "c3", "c5"],
                     help="c2: BASELINE metric (default, PESQ-wb + STOI/ESTOI); pesq: configs[1] as stated, "
                          "PESQ-wb only; c3: STOI+ESTOI only, 8192 x 5 s @ 16 kHz per GPU; "
                          "c5: config 5, mixed 8/16 kHz ragged 2-30 s batch")
@@ -338,7 +339,8 @@ def run_pesq(args, world, rank, dev, distributed):
     from fast_speech_enhancement_metrics_amd.synthetic import speech_like_pairs
     B, L = 4096, 160000
     clean, noisy, _ = speech_like_pairs(B, L, 16000, seed=42 + rank, device=dev)
-    aligned = args.workload == "pesq_aligned"
+    aligned = args.workload in ("pesq_aligned", "pesq_aligned_utt")
+    mode = "utterance" if args.workload == "pesq_aligned_utt" else "row"
     if aligned:
         # extension (not in the reference): degraded rows delayed by U[-2000, 2000] samples,
         # PESQ(time_align=True) estimates and undoes the delay before scoring (alignment.py)
@@ -348,7 +350,7 @@ def run_pesq(args, world, rank, dev, distributed):
         src = torch.arange(L, device=dev)[None, :] - delay[:, None]
         noisy = torch.where((src >= 0) & (src < L), noisy.gather(1, src.clamp(0, L - 1)), torch.zeros_like(noisy))
         del src
-    pesq = PESQ(16000, use_gpu=True, time_align=aligned)
+    pesq = PESQ(16000, use_gpu=True, time_align=mode if aligned else False)
 
     def step():
         p = pesq.scores(clean, noisy)
@@ -359,14 +361,15 @@ def run_pesq(args, world, rank, dev, distributed):
         found = int((pesq.last_delays.long() == delay).sum())
     if rank == 0:
         line = {
-            "metric": ("utterances/sec PESQ-wb with time alignment (extension), 10s@16kHz, batch 4096" if aligned
+            "metric": (f"utterances/sec PESQ-wb with time alignment ({mode} mode, extension), 10s@16kHz, batch 4096"
+                       if aligned
                        else "utterances/sec PESQ-wb, 10s@16kHz, batch 4096 (config 2)"),
             "value": round(world * B * args.steps / dt, 2), "unit": "utterances/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic speech-like pairs" + (", degraded rows delayed by U[-2000, 2000] samples" if aligned
                                                      else ""),
-            "config": {"workload": ("PESQ(16000, use_gpu=True, time_align=True).scores" if aligned
+            "config": {"workload": (f"PESQ(16000, use_gpu=True, time_align={mode!r}).scores" if aligned
                                     else "config 2: PESQ-wb scores (PESQ.scores)"), "batch_per_gpu": B,
                        "length": L, "sample_rate": 16000, "parallelism": f"dp{world}"}}
         if aligned:
@@ -511,8 +514,9 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    if args.workload in ("pesq", "pesq_aligned", "c3", "c5"):
-        {"pesq": run_pesq, "pesq_aligned": run_pesq, "c3": run_c3, "c5": run_c5}[args.workload](
+    if args.workload in ("pesq", "pesq_aligned", "pesq_aligned_utt", "c3", "c5"):
+        {"pesq": run_pesq, "pesq_aligned": run_pesq, "pesq_aligned_utt": run_pesq, "c3": run_c3,
+         "c5": run_c5}[args.workload](
             args, world, rank, dev, distributed)
         if distributed:
             dist.barrier()

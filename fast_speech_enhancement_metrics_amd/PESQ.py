@@ -32,14 +32,18 @@ class PESQ(BaseMetric):
     higher_is_better = True
     EXPECTED_SAMPLING_RATE = 16000
 
-    def __init__(self, sample_rate: int = 16000, use_gpu: bool = False, *, time_align: bool = False,
+    def __init__(self, sample_rate: int = 16000, use_gpu: bool = False, *, time_align=False,
                  max_delay: int = 16000, devices=None):
         """``time_align`` (extension, off by default as in the reference, PESQ.py:19-22): shift each
         degraded row by its estimated delay before scoring (``alignment.time_align``, P.862-style;
-        ``max_delay`` samples at 16 kHz bounds the search).  The delays of the last scored batch
+        ``max_delay`` samples at 16 kHz bounds the search): True or "row" -- one delay per row;
+        "utterance" -- P.862's per-utterance delays, the row realigned segment by segment.  The
+        delays of the last scored batch (per row; in utterance mode each row's longest segment's)
         are kept in ``last_delays``.  ``devices``: see BaseMetric (multi-device calls)."""
         super().__init__(sample_rate, use_gpu, devices=devices)
-        self.time_align = bool(time_align)
+        if time_align not in (False, True, "row", "utterance"):
+            raise ValueError('time_align must be False, True, "row" or "utterance"')
+        self.time_align = "row" if time_align is True else time_align
         self.max_delay = int(max_delay)
         self.last_delays = None
 
@@ -276,7 +280,7 @@ class PESQ(BaseMetric):
             raise Exception("`clean_speech` and `denoised_speech` should have the same shape.")
         if getattr(self, "time_align", False):
             from .alignment import time_align
-            noisy, delays = time_align(clean, noisy, lengths, self.max_delay)
+            noisy, delays = time_align(clean, noisy, lengths, self.max_delay, mode=self.time_align)
         lib = _native.load() if clean.is_cuda else None
         if lib is None:
             if lengths is None:

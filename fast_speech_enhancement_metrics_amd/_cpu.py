@@ -381,6 +381,126 @@ def time_align_row(ref: np.ndarray, deg: np.ndarray, max_delay: int) -> int:
     return d0 - _TA_FINE + i if i >= 0 else d0
 
 
+# utterance mode (csrc/align.hip stages 5-9; P.862 sections 10.3-10.5)
+_TA_MINSPEECH, _TA_JOIN, _TA_MINUTT, _TA_SEARCH, _TA_MAXU, _TA_CHUNK = 4, 50, 50, 75, 16, 5120
+_TA_SPLIT_GAIN, _TA_SPLIT_MIN = 1.2, 16
+
+
+def _ta_utterances(env: np.ndarray) -> list:
+    """[(start, end)] frames: speech runs from MINSPEECH frames, joined across gaps < JOIN, kept
+    from MINUTT, at most MAXU."""
+    act = np.flatnonzero(env > 0)
+    utt = []
+    if act.size:
+        cut = np.flatnonzero(np.diff(act) > 1)
+        rs = np.concatenate([[act[0]], act[cut + 1]])
+        re = np.concatenate([act[cut] + 1, [act[-1] + 1]])
+        keep = re - rs >= _TA_MINSPEECH
+        rs, re = rs[keep], re[keep]
+        if rs.size:
+            cut = np.flatnonzero(rs[1:] - re[:-1] >= _TA_JOIN)  # a gap of JOIN or more starts a new run
+            starts = np.concatenate([[rs[0]], rs[cut + 1]])
+            ends = np.concatenate([re[cut], [re[-1]]])
+            utt = [(int(a), int(b)) for a, b in zip(starts, ends) if b - a >= _TA_MINUTT]
+    if len(utt) > _TA_MAXU:
+        utt = utt[:_TA_MAXU - 1] + [(utt[_TA_MAXU - 1][0], utt[-1][1])]
+    return utt
+
+
+def _ta_piece_xcorr(wr, wd, a: int, b: int, lo: int, hi: int) -> np.ndarray:
+    """c[D - lo] = sum over n in [a, b) of wr[n] wd[n + D], lo <= D <= hi (wd zero outside)."""
+    L = wd.shape[0]
+    win = np.zeros(b - a + hi - lo)
+    s0 = a + lo
+    i0, i1 = max(s0, 0), min(s0 + win.shape[0], L)
+    if i1 > i0:
+        win[i0 - s0:i1 - s0] = wd[i0:i1]
+    return _xcorr_window(wr[a:b], win, 0, hi - lo) if b > a else np.zeros(hi - lo + 1)
+
+
+def time_align_utt_row(ref: np.ndarray, deg: np.ndarray, max_delay: int):
+    """(seg_start [n+1], seg_delay [n], row delay) of one row (csrc/align.hip, utterance mode)."""
+    r = np.asarray(ref, dtype=np.float64)
+    d = np.asarray(deg, dtype=np.float64)
+    L = r.shape[0]
+    er, ed = _ta_envelope(r), _ta_envelope(d)
+    nfr = er.shape[0]
+    M = min(-(-max_delay // _TA_FRAME), nfr - 1) if nfr >= 2 else 0
+    jrow = 0
+    if nfr >= 2:
+        i = _first_max(_xcorr_window(er, ed, -M, M))
+        jrow = i - M if i >= 0 else 0
+    utt = _ta_utterances(er)
+    R = [0] + [_TA_FRAME * ((utt[u - 1][1] + utt[u][0]) // 2) for u in range(1, len(utt))] + [L]
+    wins = utt if utt else [(0, nfr)]
+    wr = np.zeros(L)
+    wd = np.zeros(L)
+    wr[1:] = np.diff(r)
+    wd[1:] = np.diff(d)
+    starts, delays = [], []
+    for u, (s, e) in enumerate(wins):
+        k0, k1 = max(0, s - _TA_SEARCH), min(nfr, e + _TA_SEARCH)
+        jlo, jhi = max(-M, jrow - _TA_SEARCH), min(M, jrow + _TA_SEARCH)
+        best, arg = 0.0, None
+        for j in range(jlo, jhi + 1):
+            ks, ke = max(k0, -j), min(k1, nfr - j)
+            c = float(np.dot(er[ks:ke], ed[ks + j:ke + j])) if ke > ks else 0.0
+            if c > best:
+                best, arg = c, j
+        d0 = _TA_FRAME * (arg if arg is not None else jrow)
+        m = max(1, -(-(R[u + 1] - R[u]) // _TA_CHUNK))
+        P = np.stack([_ta_piece_xcorr(wr, wd, R[u] + i * _TA_CHUNK, min(R[u] + (i + 1) * _TA_CHUNK, R[u + 1]),
+                                      d0 - _TA_FINE, d0 + _TA_FINE) for i in range(m)])
+        W = P.sum(axis=0)
+        iW = _first_max(W)
+        segs = [(0, d0 - _TA_FINE + iW if iW >= 0 else d0)]
+        if m >= 4:
+            left = np.cumsum(P, axis=0)
+            cand = []
+            for sp in range(2, m - 1):
+                lf, rt = left[sp - 1], W - left[sp - 1]
+                iL, iR = _first_max(lf), _first_max(rt)
+                vL, vR = (lf[iL] if iL >= 0 else 0.0), (rt[iR] if iR >= 0 else 0.0)
+                cand.append((vL + vR, sp, vL, iL, vR, iR))
+            tot, sp, vL, iL, vR, iR = max(cand, key=lambda t: t[0])  # first maximum
+            vW = W[iW] if iW >= 0 else 0.0
+            if vL > 0 and vR > 0 and tot > _TA_SPLIT_GAIN * vW and abs(iL - iR) >= _TA_SPLIT_MIN:
+                segs = [(0, d0 - _TA_FINE + iL), (sp * _TA_CHUNK, d0 - _TA_FINE + iR)]
+        for off, D in segs:
+            if not (delays and delays[-1] == D):
+                starts.append(R[u] + off)
+                delays.append(D)
+    starts.append(L)
+    lens = np.diff(starts)
+    return np.array(starts), np.array(delays), int(delays[int(np.argmax(lens))])
+
+
+def time_align_utterances(clean: torch.Tensor, noisy: torch.Tensor, lengths=None, max_delay: int = 16000):
+    """(aligned [B, L] f32, delays [B], n_seg [B], seg_start [B, 33], seg_delay [B, 32]) int32."""
+    c = clean.detach().cpu().numpy()
+    n = noisy.detach().cpu().numpy()
+    B, L = c.shape
+    S = 2 * _TA_MAXU
+    out = np.zeros((B, L), dtype=np.float32)
+    ds = np.zeros(B, dtype=np.int32)
+    ns = np.zeros(B, dtype=np.int32)
+    st = np.zeros((B, S + 1), dtype=np.int32)
+    sd = np.zeros((B, S), dtype=np.int32)
+    rows = [L if lengths is None else int(min(max(int(lengths[b]), 0), L)) for b in range(B)]
+    res = _host_map(lambda b: time_align_utt_row(c[b, :rows[b]], n[b, :rows[b]], max_delay), range(B))
+    for b, (starts, delays, D) in enumerate(res):
+        k = len(delays)
+        ns[b], ds[b] = k, D
+        st[b, :k + 1] = starts
+        sd[b, :k] = delays
+        for i in range(k):
+            a, e, Dk = int(starts[i]), int(starts[i + 1]), int(delays[i])
+            lo, hi = max(a, -Dk), min(e, rows[b] - Dk)
+            if hi > lo:
+                out[b, lo:hi] = n[b, lo + Dk:hi + Dk]
+    return tuple(torch.from_numpy(x) for x in (out, ds, ns, st, sd))
+
+
 def time_align(clean: torch.Tensor, noisy: torch.Tensor, lengths=None, max_delay: int = 16000):
     """(aligned noisy [B, L] float32, delays [B] int32) of 16 kHz rows (rows past lengths[b] 0)."""
     c = clean.detach().cpu().numpy()

@@ -13,8 +13,16 @@ degraded row shifted back by it:
 * ``delay > 0``: the degraded row lags, ``deg[n] ~ ref[n - delay]``; the aligned row is
   ``deg[n + delay]`` inside the row, zero elsewhere.
 
-GPU rows run ``fsem_time_align_f32`` (``csrc/align.hip``); CPU rows the float64 FFT form in
-``_cpu.py``.  Parity against P.862 implementations is unpinned (none is importable here); the
+``mode="utterance"`` (``time_align_segments``) follows P.862's per-utterance structure instead
+(sections 10.3-10.5): the reference's utterances (speech runs of 16 ms or more joined across gaps under 200 ms,
+at least 200 ms long, at most 16 per row) own the row's regions (boundaries in the middle of the
+gaps); each gets its own crude delay (its envelope +-300 ms, within 300 ms of the row's crude
+delay) and fine delay (as above, over its region), and a region splits once where a delay
+change within it raises the summed correlation peak by 20 %.  The degraded row is realigned
+segment by segment; ``delays`` is then each row's longest segment's delay.
+
+GPU rows run ``fsem_time_align_f32`` / ``fsem_time_align_utt_f32`` (``csrc/align.hip``); CPU rows
+the float64 FFT form in ``_cpu.py``.  Parity against P.862 implementations is unpinned (none is importable here); the
 tests pin both paths to ``oracle/align_oracle.py`` and to known synthetic delays.
 """
 from __future__ import annotations
@@ -27,38 +35,90 @@ from .base import as_rows, device_lengths
 DEFAULT_MAX_DELAY = 16000  # samples at 16 kHz (1 s)
 
 
-def time_align(clean: torch.Tensor, noisy: torch.Tensor, lengths=None,
-               max_delay: int = DEFAULT_MAX_DELAY) -> tuple[torch.Tensor, torch.Tensor]:
-    """(aligned noisy [B, L] float32, delays [B] int32) of 16 kHz rows, on the rows' device.
+MODES = ("row", "utterance")
 
-    ``lengths`` (optional [B] ints): row b holds lengths[b] samples; the aligned row is zero
-    past them.  ``max_delay``: the crude search range in samples (rounded up to 4 ms frames).
-    """
+
+def _prepare(clean, noisy, max_delay):
     c = as_rows(clean)
     n = as_rows(noisy)
     if c.shape != n.shape:
         raise Exception("`clean_speech` and `denoised_speech` should have the same shape.")
     if max_delay < 0:
         raise ValueError("max_delay must be >= 0")
-    max_delay = min(int(max_delay), 2**31 - 1)  # the C-ABI's int32
-    B, L = c.shape
-    if not c.is_cuda:
-        lens = None if lengths is None else device_lengths(lengths, B, L, "cpu")
-        return _cpu.time_align(c, n, lens, int(max_delay))
-    lib = _native.load()
-    lens = device_lengths(lengths, B, L, c.device) if lengths is not None else None
+    return c, n, min(int(max_delay), 2**31 - 1)  # the C-ABI's int32
+
+
+def _device_rows(c, n):
+    """float32 rows as the C-ABI reads them: 16-byte aligned, one stride, L % 4 == 0."""
+    L = c.shape[1]
     c = c.float()
     n = n.float()
     if (c.stride(0) % 4 or n.stride(0) != c.stride(0) or L % 4 or c.data_ptr() % 16 or n.data_ptr() % 16
             or not (c.is_contiguous() and n.is_contiguous())):
-        pad = (-L) % 4  # 16-byte aligned rows read in 16-byte pieces, one stride (include/fsem.h)
+        pad = (-L) % 4
         c = torch.nn.functional.pad(c, (0, pad)).contiguous()
         n = torch.nn.functional.pad(n, (0, pad)).contiguous()
+    return c, n
+
+
+def time_align(clean: torch.Tensor, noisy: torch.Tensor, lengths=None,
+               max_delay: int = DEFAULT_MAX_DELAY, mode: str = "row") -> tuple[torch.Tensor, torch.Tensor]:
+    """(aligned noisy [B, L] float32, delays [B] int32) of 16 kHz rows, on the rows' device.
+
+    ``lengths`` (optional [B] ints): row b holds lengths[b] samples; the aligned row is zero
+    past them.  ``max_delay``: the crude search range in samples (rounded up to 4 ms frames).
+    ``mode``: "row" (one delay per row) or "utterance" (per-utterance delays, see
+    ``time_align_segments``; ``delays`` = each row's longest segment's delay).
+    """
+    if mode not in MODES:
+        raise ValueError(f"mode must be one of {MODES}")
+    if mode == "utterance":
+        out, delays, *_ = time_align_segments(clean, noisy, lengths, max_delay)
+        return out, delays
+    c, n, max_delay = _prepare(clean, noisy, max_delay)
+    B, L = c.shape
+    if not c.is_cuda:
+        lens = None if lengths is None else device_lengths(lengths, B, L, "cpu")
+        return _cpu.time_align(c, n, lens, max_delay)
+    lib = _native.load()
+    lens = device_lengths(lengths, B, L, c.device) if lengths is not None else None
+    c, n = _device_rows(c, n)
     out = torch.empty(B, L + (-L) % 4, dtype=torch.float32, device=c.device)[:, :L]  # float4 row stores
     delays = torch.empty(B, dtype=torch.int32, device=c.device)
     ws = _native.workspace(lib.fsem_time_align_workspace_bytes(B, L), c.device)
     _native.check(lib.fsem_time_align_f32(c.data_ptr(), n.data_ptr(), B, L, c.stride(0),
-                                          lens.data_ptr() if lens is not None else None, int(max_delay),
+                                          lens.data_ptr() if lens is not None else None, max_delay,
                                           delays.data_ptr(), out.data_ptr(), out.stride(0), ws.data_ptr(),
                                           ws.numel(), _native.stream_handle(c.device)), "time alignment")
     return out, delays
+
+
+def time_align_segments(clean: torch.Tensor, noisy: torch.Tensor, lengths=None,
+                        max_delay: int = DEFAULT_MAX_DELAY):
+    """Per-utterance alignment (P.862 sections 10.3-10.5, see the module docstring) of 16 kHz rows.
+
+    Returns (aligned [B, L] float32, delays [B], n_seg [B], seg_start [B, 33], seg_delay [B, 32])
+    on the rows' device (int32 but ``aligned``): segment k of row b covers samples
+    [seg_start[b, k], seg_start[b, k + 1]) for k < n_seg[b] and is shifted by seg_delay[b, k];
+    ``delays`` is each row's longest segment's delay.
+    """
+    c, n, max_delay = _prepare(clean, noisy, max_delay)
+    B, L = c.shape
+    if not c.is_cuda:
+        lens = None if lengths is None else device_lengths(lengths, B, L, "cpu")
+        return _cpu.time_align_utterances(c, n, lens, max_delay)
+    lib = _native.load()
+    lens = device_lengths(lengths, B, L, c.device) if lengths is not None else None
+    c, n = _device_rows(c, n)
+    S = _native.ALIGN_MAX_SEGMENTS
+    out = torch.empty(B, L + (-L) % 4, dtype=torch.float32, device=c.device)[:, :L]
+    i32 = dict(dtype=torch.int32, device=c.device)
+    delays, nseg = torch.empty(B, **i32), torch.empty(B, **i32)
+    starts, sdel = torch.zeros(B, S + 1, **i32), torch.zeros(B, S, **i32)
+    ws = _native.workspace(lib.fsem_time_align_utt_workspace_bytes(B, L), c.device)
+    _native.check(lib.fsem_time_align_utt_f32(c.data_ptr(), n.data_ptr(), B, L, c.stride(0),
+                                              lens.data_ptr() if lens is not None else None, max_delay,
+                                              delays.data_ptr(), nseg.data_ptr(), starts.data_ptr(),
+                                              sdel.data_ptr(), out.data_ptr(), out.stride(0), ws.data_ptr(),
+                                              ws.numel(), _native.stream_handle(c.device)), "time alignment")
+    return out, delays, nseg, starts, sdel

@@ -11,6 +11,18 @@
 //      largest cross-correlation of the signals' first differences, over the whole row;
 //   4. ta_shift: the aligned degraded row a[n] = deg[n + D] (0 <= n + D < L_row), else 0.
 // Delay D > 0: the degraded row lags the clean one, deg[n] ~ ref[n - D].
+// Utterance mode (fsem_time_align_utt_f32, P.862 sections 10.3-10.5 as restated in the oracle):
+//   5. ta_utterances: the reference's utterances (speech runs >= 16 ms joined across gaps < 200 ms, at
+//      least 200 ms long, at most 16), the regions they own (boundaries in the gaps' middles) and
+//      the regions' 5120-sample pieces;
+//   6. ta_crude_utt: each utterance's envelope lag over its search window (+-300 ms around it),
+//      within +-75 frames of the row's crude lag;
+//   7. ta_fine_partial (utterance pieces): the first-difference correlation per piece around the
+//      utterance's crude delay;
+//   8. ta_pick_utt: each region's fine delay, or two delays when splitting it at a piece boundary
+//      raises the summed correlation peak by 20 % and the halves' delays differ by >= 16 samples;
+//      ta_segments: the row's segments (equal neighbours merged) and its longest segment's delay;
+//   9. ta_shift_seg: a[n] = deg[n + D_k] in segment k.
 //
 // Cost is set by stage 3: 767 lags x L multiply-adds per row (about 123 M for 10 s), as
 // register-blocked packed FMAs out of LDS (16 consecutive lags per lane sliding over the chunk);
@@ -32,6 +44,15 @@ constexpr int CS = NSL * SL;         // samples per chunk (5120)
 constexpr int WIN = CS + NGRP * LG;  // degraded window per chunk (5888)
 static_assert(NGRP * LG >= NLAG && NGRP * NSL <= 256, "fine-stage thread map");
 constexpr int ENV_LDS = 6144;        // envelope frames per signal kept in LDS by ta_crude
+// utterance mode (oracle/align_oracle.py steps 5-9; P.862 constant names)
+constexpr int MINSPEECH = 4;         // frames: shorter speech runs are discarded (MINSPEECHLGTH)
+constexpr int JOIN = 50;             // frames: shorter gaps join two speech runs (JOINSPEECHLGTH)
+constexpr int MINUTT = 50;           // frames: shorter joined runs are not utterances
+constexpr int SEARCHBUF = 75;        // frames: crude search window margin and lag range
+constexpr int MAXU = 16;             // utterances per row
+constexpr int MAXSEG = 2 * MAXU;     // segments per row (include/fsem.h FSEM_ALIGN_MAX_SEGMENTS)
+constexpr int SPLIT_MIN = 16;        // samples: least delay difference of a split
+constexpr double SPLIT_GAIN = 1.2;   // least gain of the summed correlation peaks of a split
 
 __device__ __forceinline__ int64_t row_len(const int32_t *lengths, int64_t b, int64_t L) {
   if (!lengths) return L;
@@ -177,11 +198,20 @@ __global__ void __launch_bounds__(256) ta_crude(int64_t B, int64_t L, const int3
 // of earlier CDNA parts; gfx950's 160 KB LDS per CU holds two such workgroups.
 constexpr size_t kFineLds = sizeof(float) * (CS + (WIN + WIN / 32 + 64) + NSL * NGRP * LG);
 static_assert(kFineLds <= 80 * 1024, "ta_fine_partial: two workgroups per CU in gfx950's 160 KB of LDS");
+// Utterance mode (utt != nullptr): slot c of row b is piece i of utterance u (pieces of u are
+// slots [cs[u], cs[u+1])): samples [reg[u] + i CS, min(reg[u] + (i+1) CS, reg[u+1])) at lags
+// around that utterance's crude delay (ucrude[u]).
+struct UttTables {
+  const int *nutt;    // [B]
+  const int *reg;     // [B][MAXU + 1] region starts (samples)
+  const int *cs;      // [B][MAXU + 1] first piece slot per utterance
+  const int *ucrude;  // [B][MAXU] crude delay (samples)
+};
 __global__ void __launch_bounds__(256) ta_fine_partial(const float *__restrict__ ref, const float *__restrict__ deg,
                                                        int64_t B, int64_t L, int64_t ld,
                                                        const int32_t *__restrict__ lengths,
                                                        const int *__restrict__ crude, int nchunk,
-                                                       float *__restrict__ part) {
+                                                       float *__restrict__ part, UttTables ut) {
   __shared__ float wr[CS];
   __shared__ float wd[WIN + WIN / 32 + 64];
   __shared__ float ps[NSL][NGRP * LG];
@@ -190,14 +220,25 @@ __global__ void __launch_bounds__(256) ta_fine_partial(const float *__restrict__
   const int c = (int)(blk % nchunk);
   if (b >= B) return;
   const int64_t Lr = row_len(lengths, b, L);
-  const int64_t n0 = (int64_t)c * CS;
-  const int64_t lag0 = (int64_t)crude[b] - FINE;
+  int64_t n0 = (int64_t)c * CS, hi = n0 + CS;
+  int64_t lag0 = (int64_t)crude[b] - FINE;
+  if (ut.nutt) {
+    const int U = ut.nutt[b];
+    const int *cs = ut.cs + b * (MAXU + 1);
+    if (c >= cs[U]) return;  // past the row's pieces (uniform)
+    int u = 0;
+    while (u + 1 < U && cs[u + 1] <= c) ++u;
+    const int *reg = ut.reg + b * (MAXU + 1);
+    n0 = (int64_t)reg[u] + (int64_t)(c - cs[u]) * CS;
+    hi = std::min<int64_t>(n0 + CS, reg[u + 1]);
+    lag0 = (int64_t)ut.ucrude[b * MAXU + u] - FINE;
+  }
   const float *x = ref + b * ld, *y = deg + b * ld;
   const int tid = threadIdx.x;
   auto dif = [Lr](const float *z, int64_t i) {  // first difference, 0 outside [1, L_row)
     return (i >= 1 && i < Lr) ? z[i] - z[i - 1] : 0.f;
   };
-  for (int i = tid; i < CS; i += 256) wr[i] = dif(x, n0 + i);
+  for (int i = tid; i < CS; i += 256) wr[i] = (n0 + i < hi) ? dif(x, n0 + i) : 0.f;
   for (int i = tid; i < WIN + 32; i += 256) wd[skew(i)] = dif(y, n0 + lag0 + i);  // +32: last slides
   __syncthreads();
   const int g = tid % NGRP, sl = tid / NGRP;
@@ -312,6 +353,278 @@ __global__ void __launch_bounds__(256) ta_shift(const float *__restrict__ deg, i
   }
 }
 
+// ---------------------------------------------------------------- stage 5: utterances
+// One thread per row: a sequential pass over the reference envelope (speech runs of MINSPEECH
+// frames or more, joined across gaps < JOIN frames, kept from MINUTT frames, at most MAXU: later
+// ones join the last), then the
+// regions (boundary: the middle of the gap, in whole frames) and their pieces.  No utterance:
+// one covering the row (its crude window: every frame).
+__global__ void __launch_bounds__(64) ta_utterances(int64_t B, int64_t L, const int32_t *__restrict__ lengths,
+                                                    const float *__restrict__ E, int64_t nfr_cap,
+                                                    int *__restrict__ nutt, int *__restrict__ utt,
+                                                    int *__restrict__ reg, int *__restrict__ cs) {
+  const int64_t b = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (b >= B) return;
+  const int64_t Lr = row_len(lengths, b, L);
+  const int nfr = (int)(Lr / FRAME);
+  const float *env = E + b * nfr_cap;
+  int *us = utt + b * (2 * MAXU);
+  int n = 0, s0 = -1, e0 = -1, rs = -1;  // joined run [s0, e0), raw run from rs
+  auto flush = [&]() {
+    if (s0 >= 0 && e0 - s0 >= MINUTT) {
+      if (n < MAXU) {
+        us[2 * n] = s0;
+        us[2 * n + 1] = e0;
+        ++n;
+      } else {
+        us[2 * (MAXU - 1) + 1] = e0;
+      }
+    }
+  };
+  for (int k = 0; k <= nfr; ++k) {
+    if (k < nfr && env[k] > 0.f) {
+      if (rs < 0) rs = k;
+      continue;
+    }
+    if (rs >= 0 && k - rs >= MINSPEECH) {  // the raw run [rs, k) counts
+      if (s0 >= 0 && rs - e0 < JOIN) {
+        e0 = k;
+      } else {
+        flush();
+        s0 = rs;
+        e0 = k;
+      }
+    }
+    rs = -1;
+  }
+  flush();
+  if (n == 0) {
+    us[0] = 0;
+    us[1] = nfr;
+    n = 1;
+  }
+  nutt[b] = n;
+  int *rg = reg + b * (MAXU + 1);
+  int *c = cs + b * (MAXU + 1);
+  rg[0] = 0;
+  for (int u = 1; u < n; ++u) rg[u] = FRAME * ((us[2 * u - 1] + us[2 * u]) / 2);
+  rg[n] = (int)Lr;
+  c[0] = 0;
+  for (int u = 0; u < n; ++u) c[u + 1] = c[u] + std::max(1, (rg[u + 1] - rg[u] + CS - 1) / CS);
+}
+
+// First-maximum argmax over a 256-thread workgroup: (v, j) with v > 0, or (0, INT32_MAX).
+__device__ __forceinline__ void block_argmax(double &v, int &j, double *sv, int *sj) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const double v2 = __shfl_xor(v, off, 64);
+    const int j2 = __shfl_xor(j, off, 64);
+    if (v2 > v || (v2 == v && j2 < j)) {
+      v = v2;
+      j = j2;
+    }
+  }
+  const int w = threadIdx.x >> 6;
+  __syncthreads();  // the previous call's readers are done
+  if ((threadIdx.x & 63) == 0) {
+    sv[w] = v;
+    sj[w] = j;
+  }
+  __syncthreads();
+  v = sv[0];
+  j = sj[0];
+#pragma unroll
+  for (int q = 1; q < 4; ++q)
+    if (sv[q] > v || (sv[q] == v && sj[q] < j)) {
+      v = sv[q];
+      j = sj[q];
+    }
+}
+
+// ---------------------------------------------------------------- stage 6: per-utterance crude
+// Workgroup (utterance u, row b): lag j = jrow - SEARCHBUF + tid (within |j| <= M), the envelope
+// correlation over reference frames [start - SEARCHBUF, end + SEARCHBUF), k ascending in float.
+__global__ void __launch_bounds__(256) ta_crude_utt(int64_t B, int64_t L, const int32_t *__restrict__ lengths,
+                                                    const float *__restrict__ E, int64_t nfr_cap, int max_frames,
+                                                    const int *__restrict__ crude, const int *__restrict__ nutt,
+                                                    const int *__restrict__ utt, int *__restrict__ ucrude) {
+  __shared__ double sv[4];
+  __shared__ int sj[4];
+  const int u = blockIdx.x;
+  const int64_t b = blockIdx.y + (int64_t)blockIdx.z * 65535;
+  if (b >= B || u >= nutt[b]) return;
+  const int nfr = (int)(row_len(lengths, b, L) / FRAME);
+  const int M = nfr < 2 ? 0 : min(max_frames, nfr - 1);
+  const int jrow = crude[b] / FRAME;
+  const int jlo = max(-M, jrow - SEARCHBUF), jhi = min(M, jrow + SEARCHBUF);
+  const int k0 = max(0, utt[b * 2 * MAXU + 2 * u] - SEARCHBUF);
+  const int k1 = min(nfr, utt[b * 2 * MAXU + 2 * u + 1] + SEARCHBUF);
+  const float *r = E + b * nfr_cap, *d = E + (B + b) * nfr_cap;
+  const int j = jlo + (int)threadIdx.x;
+  double best = 0.0;
+  int arg = INT32_MAX;
+  if (j <= jhi) {
+    const int ks = max(k0, -j), ke = min(k1, nfr - j);
+    float c = 0.f;
+    for (int k = ks; k < ke; ++k) c = fmaf(r[k], d[k + j], c);
+    if (c > 0.f) {
+      best = c;
+      arg = j;
+    }
+  }
+  block_argmax(best, arg, sv, sj);
+  if (threadIdx.x == 0) ucrude[b * MAXU + u] = FRAME * (arg == INT32_MAX ? jrow : arg);
+}
+
+// ---------------------------------------------------------------- stage 8: per-utterance pick
+// Workgroup (utterance u, row b): lags l = tid + 256 q (q < 3, l < NLAG), the region's pieces
+// added in piece order (double); the whole region's first peak, then every split s in
+// [2, m - 2] (left = pieces < s, right = total - left) with two argmax reductions.
+// useg[b][u] = {segments (1 or 2), split offset (samples), delay 1, delay 2}.
+__global__ void __launch_bounds__(256) ta_pick_utt(int64_t B, const int *__restrict__ nutt, const int *__restrict__ cs,
+                                                   const int *__restrict__ ucrude, int nslot,
+                                                   const float *__restrict__ part, int *__restrict__ useg) {
+  __shared__ double sv[4];
+  __shared__ int sj[4];
+  const int u = blockIdx.x;
+  const int64_t b = blockIdx.y + (int64_t)blockIdx.z * 65535;
+  if (b >= B || u >= nutt[b]) return;
+  const int tid = threadIdx.x;
+  const int c0 = cs[b * (MAXU + 1) + u], m = cs[b * (MAXU + 1) + u + 1] - c0;
+  const float *P = part + (b * nslot + c0) * (int64_t)(NGRP * LG);
+  const int d0 = ucrude[b * MAXU + u];
+  double tot[3], left[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+  for (int q = 0; q < 3; ++q) tot[q] = 0.0;
+  for (int i = 0; i < m; ++i)
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int l = tid + 256 * q;
+      if (l < NLAG) tot[q] += P[i * (NGRP * LG) + l];
+    }
+  // the thread's first peak (lags ascending) of an array given per q
+  auto local_peak = [&](const double *a, double &v, int &j) {
+    v = 0.0;
+    j = INT32_MAX;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int l = tid + 256 * q;
+      if (l < NLAG && a[q] > v) {
+        v = a[q];
+        j = l;
+      }
+    }
+  };
+  double vW;
+  int iW;
+  local_peak(tot, vW, iW);
+  block_argmax(vW, iW, sv, sj);
+  double bestT = -1.0, bvL = 0.0, bvR = 0.0;
+  int bs = -1, biL = INT32_MAX, biR = INT32_MAX;
+  for (int s = 1; s + 1 < m && m >= 4; ++s) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int l = tid + 256 * q;
+      if (l < NLAG) left[q] += P[(s - 1) * (NGRP * LG) + l];
+    }
+    if (s < 2) continue;
+    double right[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) right[q] = tot[q] - left[q];
+    double vL, vR;
+    int iL, iR;
+    local_peak(left, vL, iL);
+    local_peak(right, vR, iR);
+    block_argmax(vL, iL, sv, sj);
+    block_argmax(vR, iR, sv, sj);
+    if (vL + vR > bestT) {  // uniform: every thread holds the reduced values
+      bestT = vL + vR;
+      bs = s;
+      bvL = vL;
+      bvR = vR;
+      biL = iL;
+      biR = iR;
+    }
+  }
+  if (tid == 0) {
+    int *o = useg + (b * MAXU + u) * 4;
+    const bool split = bs > 0 && bvL > 0.0 && bvR > 0.0 && bestT > SPLIT_GAIN * vW &&
+                       abs(biL - biR) >= SPLIT_MIN;
+    o[0] = split ? 2 : 1;
+    o[1] = split ? bs * CS : 0;
+    o[2] = split ? d0 - FINE + biL : (iW == INT32_MAX ? d0 : d0 - FINE + iW);
+    o[3] = split ? d0 - FINE + biR : o[2];
+  }
+}
+
+// One thread per row: the segments in order (equal neighbours merged), the row's delay (its
+// longest segment's, the first of equals).
+__global__ void __launch_bounds__(64) ta_segments(int64_t B, int64_t L, const int32_t *__restrict__ lengths,
+                                                  const int *__restrict__ nutt, const int *__restrict__ reg,
+                                                  const int *__restrict__ useg, int *__restrict__ nseg,
+                                                  int *__restrict__ seg_start, int *__restrict__ seg_delay,
+                                                  int *__restrict__ delay) {
+  const int64_t b = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (b >= B) return;
+  const int U = nutt[b];
+  const int *rg = reg + b * (MAXU + 1);
+  int *st = seg_start + b * (MAXSEG + 1), *dl = seg_delay + b * MAXSEG;
+  int n = 0;
+  auto add = [&](int start, int d) {
+    if (n > 0 && dl[n - 1] == d) return;
+    st[n] = start;
+    dl[n] = d;
+    ++n;
+  };
+  for (int u = 0; u < U; ++u) {
+    const int *o = useg + (b * MAXU + u) * 4;
+    add(rg[u], o[2]);
+    if (o[0] == 2) add(rg[u] + o[1], o[3]);
+  }
+  st[n] = (int)row_len(lengths, b, L);
+  int best = -1, d = 0;
+  for (int k = 0; k < n; ++k)
+    if (st[k + 1] - st[k] > best) {
+      best = st[k + 1] - st[k];
+      d = dl[k];
+    }
+  if (nseg) nseg[b] = n;
+  if (delay) delay[b] = d;
+}
+
+// ---------------------------------------------------------------- stage 9: segment shift
+__global__ void __launch_bounds__(256) ta_shift_seg(const float *__restrict__ deg, int64_t B, int64_t L, int64_t ld,
+                                                    const int32_t *__restrict__ lengths, const int *__restrict__ nseg,
+                                                    const int *__restrict__ seg_start,
+                                                    const int *__restrict__ seg_delay, float *__restrict__ out,
+                                                    int64_t ld_out) {
+  __shared__ int st[MAXSEG + 1], dl[MAXSEG];
+  const int64_t b = blockIdx.y + (int64_t)blockIdx.z * 65535;
+  if (b >= B) return;
+  const int n_s = nseg[b];
+  if (threadIdx.x <= n_s) st[threadIdx.x] = seg_start[b * (MAXSEG + 1) + threadIdx.x];
+  if (threadIdx.x < n_s) dl[threadIdx.x] = seg_delay[b * MAXSEG + threadIdx.x];
+  __syncthreads();
+  const int64_t n = 4 * ((int64_t)blockIdx.x * 256 + threadIdx.x);
+  if (n >= L) return;
+  const int64_t Lr = row_len(lengths, b, L);
+  const float *y = deg + b * ld;
+  int k = 0;
+  while (k + 1 < n_s && st[k + 1] <= n) ++k;
+  float v[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    while (k + 1 < n_s && st[k + 1] <= n + i) ++k;
+    const int64_t m = n + i + dl[k];
+    v[i] = (n + i < Lr && m >= 0 && m < Lr) ? y[m] : 0.f;
+  }
+  if (n + 4 <= L) {
+    *reinterpret_cast<float4 *>(out + b * ld_out + n) = make_float4(v[0], v[1], v[2], v[3]);
+  } else {
+    for (int i = 0; i < 4 && n + i < L; ++i) out[b * ld_out + n + i] = v[i];
+  }
+}
+
 inline int64_t frames_cap(int64_t L) { return L / FRAME; }
 inline int64_t nchunks(int64_t L) { return (L + CS - 1) / CS; }
 
@@ -339,6 +652,44 @@ inline Ws carve(void *ws, int64_t B, int64_t L) {
   w.delay = reinterpret_cast<int *>(p);
   p += align_up((size_t)B * 4, 256);
   w.part = reinterpret_cast<float *>(p);
+  return w;
+}
+
+// utterance mode: the row-mode arrays (E, crude, internal delay; part with nslot pieces per row)
+// plus the utterance tables and the internal segment outputs
+inline int64_t nslots(int64_t L) { return nchunks(L) + MAXU; }
+struct UttWs {
+  float *E, *part;
+  int *crude, *delay, *nutt, *utt, *reg, *cs, *ucrude, *useg, *nseg, *seg_start, *seg_delay;
+};
+inline size_t utt_ws_bytes(int64_t B, int64_t L) {
+  auto ints = [B](int64_t per_row) { return align_up((size_t)(B * per_row) * 4, 256); };
+  return align_up((size_t)(2 * B * std::max<int64_t>(frames_cap(L), 1)) * 4, 256) +
+         align_up((size_t)(B * nslots(L) * NGRP * LG) * 4, 256) + ints(1) * 4 + ints(2 * MAXU) +
+         2 * ints(MAXU + 1) + ints(MAXU) + ints(4 * MAXU) + ints(MAXSEG + 1) + ints(MAXSEG);
+}
+inline UttWs utt_carve(void *ws, int64_t B, int64_t L) {
+  char *p = static_cast<char *>(ws);
+  UttWs w;
+  auto take = [&](size_t bytes) {
+    char *q = p;
+    p += align_up(bytes, 256);
+    return q;
+  };
+  w.E = reinterpret_cast<float *>(take((size_t)(2 * B * std::max<int64_t>(frames_cap(L), 1)) * 4));
+  w.part = reinterpret_cast<float *>(take((size_t)(B * nslots(L) * NGRP * LG) * 4));
+  auto ti = [&](int64_t per_row) { return reinterpret_cast<int *>(take((size_t)(B * per_row) * 4)); };
+  w.crude = ti(1);
+  w.delay = ti(1);
+  w.nutt = ti(1);
+  w.nseg = ti(1);
+  w.utt = ti(2 * MAXU);
+  w.reg = ti(MAXU + 1);
+  w.cs = ti(MAXU + 1);
+  w.ucrude = ti(MAXU);
+  w.useg = ti(4 * MAXU);
+  w.seg_start = ti(MAXSEG + 1);
+  w.seg_delay = ti(MAXSEG);
   return w;
 }
 
@@ -382,7 +733,7 @@ extern "C" int fsem_time_align_f32(const float *ref, const float *deg, int64_t b
   align::ta_crude<<<xy(batch), 256, 0, st>>>(batch, length, lengths, w.E, nfr_cap, max_frames, w.crude);
   FSEM_CHECK_LAUNCH();
   align::ta_fine_partial<<<(unsigned)(batch * nch), 256, 0, st>>>(ref, deg, batch, length, ld, lengths, w.crude,
-                                                                  (int)nch, w.part);
+                                                                  (int)nch, w.part, align::UttTables{});
   FSEM_CHECK_LAUNCH();
   align::ta_fine_pick<<<xy(batch), 256, 0, st>>>(batch, w.crude, (int)nch, w.part, dl);
   FSEM_CHECK_LAUNCH();
@@ -390,6 +741,76 @@ extern "C" int fsem_time_align_f32(const float *ref, const float *deg, int64_t b
     dim3 grid = yz(batch);
     grid.x = (unsigned)((length + 1023) / 1024);
     align::ta_shift<<<grid, 256, 0, st>>>(deg, batch, length, ld, lengths, dl, deg_aligned, ld_out);
+    FSEM_CHECK_LAUNCH();
+  }
+  return FSEM_OK;
+}
+
+extern "C" size_t fsem_time_align_utt_workspace_bytes(int64_t batch, int64_t length) {
+  if (batch <= 0 || length <= 0) return 0;
+  return align::utt_ws_bytes(batch, length);
+}
+
+extern "C" int fsem_time_align_utt_f32(const float *ref, const float *deg, int64_t batch, int64_t length,
+                                       int64_t ld, const int32_t *lengths, int32_t max_delay, int32_t *delay,
+                                       int32_t *n_seg, int32_t *seg_start, int32_t *seg_delay,
+                                       float *deg_aligned, int64_t ld_out, void *ws, size_t ws_bytes,
+                                       void *stream) {
+  if (!ref || !deg || batch <= 0 || length <= 0 || ld < length || length > kMaxLength || max_delay < 0 ||
+      (deg_aligned && (ld_out < length || ld_out % 4 != 0)) || (ld % 4) != 0 ||
+      (!delay && !n_seg && !deg_aligned) || ((n_seg != nullptr) != (seg_start != nullptr)) ||
+      ((n_seg != nullptr) != (seg_delay != nullptr)))
+    return FSEM_EINVAL;
+  const int64_t nsl = align::nslots(length);
+  if (batch * nsl > INT32_MAX) return FSEM_EINVAL;
+  if (!ws || ws_bytes < align::utt_ws_bytes(batch, length)) return FSEM_EWORKSPACE;
+  hipStream_t st = (hipStream_t)stream;
+  align::UttWs w = align::utt_carve(ws, batch, length);
+  int *dl = delay ? delay : w.delay;
+  int *ns = n_seg ? n_seg : w.nseg;
+  int *ss = seg_start ? seg_start : w.seg_start;
+  int *sd = seg_delay ? seg_delay : w.seg_delay;
+  const int64_t nfr_cap = std::max<int64_t>(align::frames_cap(length), 1);
+  const int64_t sig = 2 * batch;
+  const int max_frames =
+      (int)std::min<int64_t>(((int64_t)max_delay + align::FRAME - 1) / align::FRAME, (int64_t)INT32_MAX);
+  auto yz = [](int64_t n) { return dim3(1, (unsigned)std::min<int64_t>(n, 65535), (unsigned)((n + 65534) / 65535)); };
+  auto xy = [](int64_t n) { return dim3((unsigned)std::min<int64_t>(n, 65535), (unsigned)((n + 65534) / 65535)); };
+  {
+    dim3 grid = yz(sig);
+    grid.x = (unsigned)((nfr_cap + 15) / 16);
+    align::ta_energy<<<grid, 256, 0, st>>>(ref, deg, batch, length, ld, lengths, w.E, nfr_cap);
+    FSEM_CHECK_LAUNCH();
+  }
+  align::ta_envelope<<<xy(sig), 256, 0, st>>>(batch, length, lengths, w.E, nfr_cap);
+  FSEM_CHECK_LAUNCH();
+  align::ta_crude<<<xy(batch), 256, 0, st>>>(batch, length, lengths, w.E, nfr_cap, max_frames, w.crude);
+  FSEM_CHECK_LAUNCH();
+  const unsigned rb = (unsigned)((batch + 63) / 64);
+  align::ta_utterances<<<rb, 64, 0, st>>>(batch, length, lengths, w.E, nfr_cap, w.nutt, w.utt, w.reg, w.cs);
+  FSEM_CHECK_LAUNCH();
+  {
+    dim3 grid = yz(batch);
+    grid.x = align::MAXU;
+    align::ta_crude_utt<<<grid, 256, 0, st>>>(batch, length, lengths, w.E, nfr_cap, max_frames, w.crude, w.nutt,
+                                              w.utt, w.ucrude);
+    FSEM_CHECK_LAUNCH();
+  }
+  align::ta_fine_partial<<<(unsigned)(batch * nsl), 256, 0, st>>>(
+      ref, deg, batch, length, ld, lengths, w.crude, (int)nsl, w.part, align::UttTables{w.nutt, w.reg, w.cs, w.ucrude});
+  FSEM_CHECK_LAUNCH();
+  {
+    dim3 grid = yz(batch);
+    grid.x = align::MAXU;
+    align::ta_pick_utt<<<grid, 256, 0, st>>>(batch, w.nutt, w.cs, w.ucrude, (int)nsl, w.part, w.useg);
+    FSEM_CHECK_LAUNCH();
+  }
+  align::ta_segments<<<rb, 64, 0, st>>>(batch, length, lengths, w.nutt, w.reg, w.useg, ns, ss, sd, dl);
+  FSEM_CHECK_LAUNCH();
+  if (deg_aligned) {
+    dim3 grid = yz(batch);
+    grid.x = (unsigned)((length + 1023) / 1024);
+    align::ta_shift_seg<<<grid, 256, 0, st>>>(deg, batch, length, ld, lengths, ns, ss, sd, deg_aligned, ld_out);
     FSEM_CHECK_LAUNCH();
   }
   return FSEM_OK;

@@ -933,4 +933,4 @@ extern "C" const char *fsem_strerror(int code) {
   }
 }
 
-extern "C" int fsem_version(void) { return 4; }  // 4: + fsem_pre_emphasize_f32; 3: + fsem_time_align_*, fsem_pesq_distances_*
+extern "C" int fsem_version(void) { return 5; }  // 5: + fsem_time_align_utt_*; 4: + fsem_pre_emphasize_f32; 3: + fsem_time_align_*, fsem_pesq_distances_*

@@ -63,7 +63,7 @@ extern "C" {
 #define FSEM_ERATE -5         /* unsupported sample-rate pair (see resampling)      */
 
 const char *fsem_strerror(int code);
-int fsem_version(void);  /* 4 since round 4 (fsem_pre_emphasize_f32); 3: time alignment, distances */
+int fsem_version(void);  /* 5: + fsem_time_align_utt_*; 4: + fsem_pre_emphasize_f32; 3: time alignment, distances */
 
 /* ---------------------------------------------------------------- resampling
  * torchaudio.transforms.Resample(orig, new) (sinc_interp_hann, width 6,
@@ -218,6 +218,31 @@ int fsem_time_align_f32(const float *ref, const float *deg, int64_t batch, int64
                         int64_t ld, const int32_t *lengths, int32_t max_delay, int32_t *delay,
                         float *deg_aligned, int64_t ld_out, void *ws, size_t ws_bytes,
                         void *stream);
+
+/* utterance mode (ABI 5): P.862's per-utterance alignment (sections 10.3-10.5, restated in
+ * oracle/align_oracle.py steps 5-9; parity against P.862 implementations unpinned):
+ *   utterances of the reference (envelope speech runs of 16 ms or more, joined across gaps < 200 ms, at
+ *   least 200 ms, at most 16 per row) each own a region of the row (boundaries in the middle of
+ *   the gaps); per utterance a crude delay (envelope correlation over the utterance +-300 ms,
+ *   within +-300 ms of the row's crude delay), then the fine delay of its region as above; a
+ *   region splits once at a 5120-sample piece boundary when two delays (>= 16 samples apart)
+ *   raise the summed correlation peak by 20 %.  Consecutive segments of equal delay are merged.
+ *   delay     : NULL or [batch] int32: the row's longest segment's delay (first of equals)
+ *   n_seg     : NULL or [batch] int32 segment counts (1 .. FSEM_ALIGN_MAX_SEGMENTS)
+ *   seg_start : NULL or [batch, FSEM_ALIGN_MAX_SEGMENTS + 1] int32: segment k of row b covers
+ *               samples [seg_start[b][k], seg_start[b][k + 1]); seg_start[b][n_seg[b]] = lengths[b]
+ *   seg_delay : NULL or [batch, FSEM_ALIGN_MAX_SEGMENTS] int32 delays (n_seg, seg_start and
+ *               seg_delay: all three or none; at least one of delay / n_seg / deg_aligned)
+ *   deg_aligned[b][n] = deg[b][n + D_k] for n in segment k where 0 <= n + D_k < lengths[b], else 0
+ * Other arguments as fsem_time_align_f32.
+ */
+#define FSEM_ALIGN_MAX_SEGMENTS 32
+size_t fsem_time_align_utt_workspace_bytes(int64_t batch, int64_t length);
+int fsem_time_align_utt_f32(const float *ref, const float *deg, int64_t batch, int64_t length,
+                            int64_t ld, const int32_t *lengths, int32_t max_delay, int32_t *delay,
+                            int32_t *n_seg, int32_t *seg_start, int32_t *seg_delay,
+                            float *deg_aligned, int64_t ld_out, void *ws, size_t ws_bytes,
+                            void *stream);
 
 #ifdef __cplusplus
 }

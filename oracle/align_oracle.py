@@ -24,6 +24,31 @@ known delay (``tests/test_align_cpu.py``, ``tests/test_align_gpu.py``):
    degraded row is a[n] = deg[n + D] where 0 <= n + D < L, else 0.
 
 Ties: the first maximum in increasing lag order.
+
+Utterance mode (``align_utterances``; engine ``fsem_time_align_utt_f32``), P.862 section 10.3-10.5
+restated with the fine stage above:
+
+5. Utterances (P.862 ``id_searchwindows`` / ``id_utterances``): runs of reference frames with a
+   positive envelope, runs shorter than MINSPEECH = 4 frames discarded (P.862's MINSPEECHLGTH);
+   runs separated by fewer than JOIN = 50 frames (200 ms) are joined, joined runs shorter than
+   MINUTT = 50 frames dropped; at most MAXU = 16 (the rest joins the 16th).
+   No utterance: the whole row is one.  Regions: utterance u owns samples [R_u, R_u+1) with
+   R_0 = 0, R_u = 64 * floor((end_u-1 + start_u) / 2) (the middle of the gap), R_U = L.
+6. Per-utterance crude delay (P.862 ``crude_align`` on the utterance's search window): the
+   envelope correlation over reference frames [start - SEARCHBUF, end + SEARCHBUF) (75 frames,
+   300 ms) at lags within SEARCHBUF frames of the row's crude lag (and |j| <= M); the row's
+   crude delay if no lag correlates positively.
+7. Per-utterance fine delay: the first-difference correlation of step 3 over the region's
+   samples, within +-383 of the utterance's crude delay, accumulated over CHUNK = 5120-sample
+   pieces of the region (from R_u).
+8. Split (P.862 ``utterance_split``, one level): a region of m >= 4 pieces is tried at every
+   piece boundary s in [2, m - 2]; left = sum of pieces < s, right = total - left; the split with
+   the largest peak(left) + peak(right) (first such s) is taken when both peaks are positive, it
+   beats the whole region's peak by SPLIT_GAIN = 1.2 and the two delays differ by at least
+   SPLIT_MIN = 16 samples (1 ms).  Segments: the regions, or their two halves, each with its
+   delay, consecutive segments of equal delay merged (at most 32 per row); the row's delay is the
+   longest segment's (the first of equals).
+9. The aligned degraded row: a[n] = deg[n + D_k] for n in segment k where 0 <= n + D_k < L.
 """
 from __future__ import annotations
 
@@ -119,3 +144,162 @@ def align(ref: np.ndarray, deg: np.ndarray, max_delay: int = 16000, lengths=None
         ds[b] = delay(ref[b, :n], deg[b, :n], max_delay)
         out[b, :n] = shift(deg[b, :n], int(ds[b]))
     return out, ds
+
+
+# ----------------------------------------------------------------------------- utterance mode
+MINSPEECH = 4     # frames: shorter speech runs are discarded (P.862 MINSPEECHLGTH)
+JOIN = 50         # frames: gaps shorter than this join two speech runs (P.862 JOINSPEECHLGTH)
+MINUTT = 50       # frames: shorter joined runs are not utterances
+SEARCHBUF = 75    # frames: the crude search window's margin around an utterance
+MAXU = 16         # utterances per row
+CHUNK = 5120      # samples per fine-stage piece (split points lie between pieces)
+SPLIT_GAIN = 1.2
+SPLIT_MIN = 16
+MAXSEG = 2 * MAXU
+
+
+def utterances(env_r: np.ndarray) -> list:
+    """Step 5: [(start, end)] frames of the reference's utterances."""
+    act = np.asarray(env_r) > 0
+    runs, k, n = [], 0, act.shape[0]
+    while k < n:
+        if act[k]:
+            e = k
+            while e < n and act[e]:
+                e += 1
+            runs.append([k, e])
+            k = e
+        else:
+            k += 1
+    joined = []
+    for s, e in (r for r in runs if r[1] - r[0] >= MINSPEECH):
+        if joined and s - joined[-1][1] < JOIN:
+            joined[-1][1] = e
+        else:
+            joined.append([s, e])
+    utt = [(s, e) for s, e in joined if e - s >= MINUTT]
+    if len(utt) > MAXU:
+        utt = utt[:MAXU - 1] + [(utt[MAXU - 1][0], utt[-1][1])]
+    return utt
+
+
+def region_starts(utt: list, L: int) -> list:
+    """Step 5: R_0 .. R_U (samples) of the utterances' regions."""
+    if not utt:
+        return [0, L]
+    return [0] + [FRAME * ((utt[u - 1][1] + utt[u][0]) // 2) for u in range(1, len(utt))] + [L]
+
+
+def crude_window(env_r: np.ndarray, env_d: np.ndarray, k0: int, k1: int, jlo: int, jhi: int) -> int | None:
+    """Step 6: lag (frames, jlo <= j <= jhi) of the largest positive correlation over reference
+    frames [k0, k1)."""
+    nfr = min(env_r.shape[0], env_d.shape[0])
+    best, arg = 0.0, None
+    for j in range(jlo, jhi + 1):
+        ks, ke = max(k0, -j), min(k1, nfr - j)
+        c = float(np.dot(env_r[ks:ke], env_d[ks + j:ke + j])) if ke > ks else 0.0
+        if c > best:
+            best, arg = c, j
+    return arg
+
+
+def fine_pieces(wr: np.ndarray, wd: np.ndarray, R0: int, R1: int, d0: int) -> np.ndarray:
+    """Step 7: P[i][l], lag d0 - FINE + l, over piece i = [R0 + i CHUNK, min(R0 + (i+1) CHUNK, R1))."""
+    L = wr.shape[0]
+    m = max(1, -(-(R1 - R0) // CHUNK))
+    P = np.zeros((m, 2 * FINE + 1))
+    for i in range(m):
+        a, b = R0 + i * CHUNK, min(R0 + (i + 1) * CHUNK, R1)
+        for li, D in enumerate(range(d0 - FINE, d0 + FINE + 1)):
+            lo, hi = max(a, 1, 1 - D), min(b, L, L - D)
+            if hi > lo:
+                P[i, li] = float(np.dot(wr[lo:hi], wd[lo + D:hi + D]))
+    return P
+
+
+def _peak(c: np.ndarray):
+    i = int(np.argmax(c))
+    return (float(c[i]), i) if c[i] > 0 else (0.0, -1)
+
+
+def pick_split(P: np.ndarray, d0: int):
+    """Step 8: [(piece offset, delay)] of one region: one segment, or two after a split."""
+    W = P.sum(axis=0)
+    vW, iW = _peak(W)
+    dW = d0 - FINE + iW if iW >= 0 else d0
+    m = P.shape[0]
+    best = None
+    if m >= 4:
+        left = np.zeros_like(W)
+        for s in range(1, m - 1):
+            left = left + P[s - 1]
+            if s < 2:
+                continue
+            vL, iL = _peak(left)
+            vR, iR = _peak(W - left)
+            if best is None or vL + vR > best[0]:
+                best = (vL + vR, s, vL, iL, vR, iR)
+    if best is not None:
+        tot, s, vL, iL, vR, iR = best
+        if vL > 0 and vR > 0 and tot > SPLIT_GAIN * vW and abs(iL - iR) >= SPLIT_MIN:
+            return [(0, d0 - FINE + iL), (s * CHUNK, d0 - FINE + iR)]
+    return [(0, dW)]
+
+
+def segments(ref: np.ndarray, deg: np.ndarray, max_delay: int = 16000):
+    """(seg_start [n+1], seg_delay [n], row delay) of one row pair (steps 5-8)."""
+    r = np.asarray(ref, dtype=np.float64)
+    d = np.asarray(deg, dtype=np.float64)
+    L = r.shape[0]
+    env_r, env_d = envelope(r), envelope(d)
+    nfr = env_r.shape[0]
+    M = min(-(-max_delay // FRAME), nfr - 1) if nfr >= 2 else 0
+    jrow = crude_delay(env_r, env_d, -(-max_delay // FRAME)) if nfr >= 2 else 0
+    utt = utterances(env_r)
+    R = region_starts(utt, L)
+    wr = np.zeros(L)
+    wd = np.zeros(L)
+    wr[1:] = np.diff(r)
+    wd[1:] = np.diff(d)
+    starts, delays = [], []
+    wins = utt if utt else [(0, nfr)]
+    for u, (s, e) in enumerate(wins):
+        j = crude_window(env_r, env_d, max(0, s - SEARCHBUF), min(nfr, e + SEARCHBUF),
+                         max(-M, jrow - SEARCHBUF), min(M, jrow + SEARCHBUF))
+        d0 = FRAME * (j if j is not None else jrow)
+        for off, D in pick_split(fine_pieces(wr, wd, R[u], R[u + 1], d0), d0):
+            if delays and delays[-1] == D:
+                continue  # merged with the previous segment
+            starts.append(R[u] + off)
+            delays.append(D)
+    starts.append(L)
+    lens = np.diff(starts)
+    return np.array(starts), np.array(delays), int(delays[int(np.argmax(lens))])
+
+
+def shift_segments(deg: np.ndarray, starts, delays) -> np.ndarray:
+    """Step 9."""
+    L = deg.shape[0]
+    out = np.zeros_like(deg)
+    for k, D in enumerate(delays):
+        a, b = int(starts[k]), int(starts[k + 1])
+        lo, hi = max(a, -D), min(b, L - D)
+        if hi > lo:
+            out[lo:hi] = deg[lo + D:hi + D]
+    return out
+
+
+def align_utterances(ref: np.ndarray, deg: np.ndarray, max_delay: int = 16000, lengths=None):
+    """(aligned [B, L], row delays [B], [(seg_start, seg_delay)] per row) for [B, L] rows."""
+    ref = np.atleast_2d(ref)
+    deg = np.atleast_2d(deg)
+    B, L = ref.shape
+    out = np.zeros_like(deg)
+    ds = np.zeros(B, dtype=np.int64)
+    segs = []
+    for b in range(B):
+        n = L if lengths is None else int(min(max(lengths[b], 0), L))
+        st, dl, ds[b] = segments(ref[b, :n], deg[b, :n], max_delay)
+        out[b, :n] = shift_segments(deg[b, :n], st, dl)
+        segs.append((st, dl))
+    return out, ds, segs

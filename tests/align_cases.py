@@ -1,0 +1,60 @@
+"""Synthetic pairs with known per-utterance delays for the utterance-mode alignment tests
+(tests/test_align_utt_cpu.py, tests/test_align_utt_gpu.py): speech-like bursts
+(fast_speech_enhancement_metrics_amd.synthetic) gated into utterances over a low noise floor;
+the degraded row shifts each utterance's region (boundaries in the middle of the gaps) by its own
+delay, optionally changing the delay inside one utterance."""
+import numpy as np
+
+from fast_speech_enhancement_metrics_amd.synthetic import speech_like_pairs
+
+
+def _shift(x: np.ndarray, D: int) -> np.ndarray:
+    """y[n] = x[n - D] inside the row, else 0."""
+    L = x.shape[0]
+    y = np.zeros_like(x)
+    lo, hi = max(0, D), min(L, L + D)
+    if hi > lo:
+        y[lo:hi] = x[lo - D:hi - D]
+    return y
+
+
+def utt_pair(seed: int, L: int, utts, delays, split=None):
+    """(clean, degraded) float32 rows.  utts: [(start, end)] samples of the utterances; delays: one
+    per utterance (D > 0: the degraded lags); split = (u, at, D2): utterance u's delay becomes D2
+    from sample ``at`` on."""
+    c, n, _ = speech_like_pairs(1, L, 16000, seed=seed, snr_low=15.0, snr_high=25.0)
+    c, n = c[0].numpy().astype(np.float64), n[0].numpy().astype(np.float64)
+    gate = np.zeros(L)
+    for s, e in utts:
+        gate[s:e] = 1.0
+    rng = np.random.default_rng(seed)
+    floor = 1e-3 * np.abs(c).max()
+    clean = c * gate + floor * rng.standard_normal(L)
+    ng = n * gate
+    deg = floor * rng.standard_normal(L)
+    bounds = [0] + [(utts[u - 1][1] + utts[u][0]) // 2 for u in range(1, len(utts))] + [L]
+    for u, D in enumerate(delays):
+        pieces = [(bounds[u], bounds[u + 1], D)]
+        if split and split[0] == u:
+            pieces = [(bounds[u], split[1], D), (split[1], bounds[u + 1], split[2])]
+        for a, b, d in pieces:
+            seg = np.zeros(L)
+            seg[a:b] = ng[a:b]
+            deg += _shift(seg, d)
+    return clean.astype(np.float32), deg.astype(np.float32)
+
+
+L_UTT = 96000
+# (utterances, delays, split, expected delays of the segments in order)
+CASES = [
+    ([(4000, 30000), (42000, 70000), (80000, 94000)], [120, -250, 900], None, [120, -250, 900]),
+    ([(3000, 60000), (70000, 90000)], [200, -40], (0, 30000, 330), [200, 330, -40]),
+    ([(2000, 40000), (52000, 92000)], [-700, -700], None, [-700]),
+    ([(6000, 88000)], [57], None, [57]),
+]
+
+
+def batch(seed0: int = 5):
+    """[B, L_UTT] clean / degraded rows of CASES (seeds seed0, seed0 + 1, ...)."""
+    rows = [utt_pair(seed0 + i, L_UTT, u, d, sp) for i, (u, d, sp, _) in enumerate(CASES)]
+    return np.stack([r[0] for r in rows]), np.stack([r[1] for r in rows])

@@ -1,0 +1,103 @@
+"""Utterance-mode time alignment on the GPU (fsem_time_align_utt_f32, csrc/align.hip stages 5-9)
+against the oracle (oracle/align_oracle.py steps 5-9; PARITY UNPINNED against P.862
+implementations -- the reference has no time alignment, PESQ.py:19-22): segments, segment
+delays, row delays equal to the oracle's and to the known per-utterance delays of
+tests/align_cases.py (a delay change inside one utterance included), aligned rows bitwise the
+oracle's segment shift, ragged and empty rows, PESQ(time_align="utterance") equal to the engine's
+PESQ of the aligned rows, and a 512 x 10 s batch of the cases' kind."""
+import time
+
+import numpy as np
+import pytest
+import torch
+
+from fast_speech_enhancement_metrics_amd.alignment import time_align, time_align_segments
+from oracle import align_oracle as A
+from tests import align_cases as AC
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    return torch.device("cuda:0")
+
+
+def _check(res, want, B):
+    al, dl, ns, st, sd = (t.cpu().numpy() for t in res)
+    out, ds, segs = want
+    np.testing.assert_array_equal(dl, ds)
+    for b in range(B):
+        s_o, d_o = segs[b]
+        k = int(ns[b])
+        np.testing.assert_array_equal(st[b, :k + 1], s_o)
+        np.testing.assert_array_equal(sd[b, :k], d_o)
+    np.testing.assert_array_equal(al, out)
+
+
+def test_engine_matches_oracle(dev):
+    c, d = AC.batch()
+    want = A.align_utterances(c, d)
+    res = time_align_segments(torch.from_numpy(c).to(dev), torch.from_numpy(d).to(dev))
+    _check(res, want, c.shape[0])
+    for (st, dl), case in zip(want[2], AC.CASES):
+        assert list(dl) == case[3]
+
+
+def test_engine_ragged_empty_and_bounded(dev):
+    c, d = AC.batch(seed0=11)
+    lens = [AC.L_UTT, 50000, 0, 700]
+    want = A.align_utterances(c, d, lengths=lens)
+    res = time_align_segments(torch.from_numpy(c).to(dev), torch.from_numpy(d).to(dev), lengths=lens)
+    _check(res, want, c.shape[0])
+    # a small max_delay bounds the crude lags (row and utterances) as in the oracle
+    want = A.align_utterances(c, d, max_delay=256)
+    res = time_align_segments(torch.from_numpy(c).to(dev), torch.from_numpy(d).to(dev), max_delay=256)
+    _check(res, want, c.shape[0])
+
+
+def test_pesq_utterance_mode(dev):
+    from fast_speech_enhancement_metrics_amd import PESQ
+    c, d = AC.batch()
+    ct, dt = torch.from_numpy(c).to(dev), torch.from_numpy(d).to(dev)
+    m = PESQ(16000, use_gpu=True, time_align="utterance")
+    got = m.scores(ct, dt)
+    al, ds = time_align(ct, dt, mode="utterance")
+    want = PESQ(16000, use_gpu=True).scores(ct, al)
+    torch.testing.assert_close(got, want, rtol=0, atol=0)
+    np.testing.assert_array_equal(m.last_delays.cpu().numpy(), A.align_utterances(c, d)[1])
+
+
+def test_engine_at_scale(dev):
+    """512 rows x 10 s, each with 4 utterances at known delays (two per row pattern): every
+    segment delay recovered; rows spot-checked against the oracle."""
+    L = 160000
+    utts = [(3000, 36000), (48000, 80000), (92000, 120000), (132000, 156000)]
+    rng = np.random.default_rng(7)
+    rows, dels = [], []
+    for b in range(64):
+        D = [int(x) for x in rng.integers(-1200, 1200, 4)]
+        rows.append(AC.utt_pair(100 + b, L, utts, D))
+        dels.append(D)
+    c = np.stack([r[0] for r in rows] * 8)
+    d = np.stack([r[1] for r in rows] * 8)
+    ct, dt = torch.from_numpy(c).to(dev), torch.from_numpy(d).to(dev)
+    time_align_segments(ct[:8], dt[:8])  # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    al, dl, ns, st, sd = time_align_segments(ct, dt)
+    torch.cuda.synchronize()
+    ms = 1e3 * (time.perf_counter() - t0)
+    print(f"utterance-mode alignment, 512 x 10 s: {ms:.2f} ms")
+    ns, sd = ns.cpu().numpy(), sd.cpu().numpy()
+    hit = 0
+    for b in range(512):
+        got = list(sd[b, :ns[b]])
+        want = [x for i, x in enumerate(dels[b % 64]) if i == 0 or x != dels[b % 64][i - 1]]
+        hit += got == want
+    assert hit >= 0.95 * 512, hit
+    for b in (0, 5, 63):
+        out, ds, segs = A.align_utterances(c[b:b + 1], d[b:b + 1])
+        np.testing.assert_array_equal(sd[b, :ns[b]], segs[0][1])
+        np.testing.assert_array_equal(al[b].cpu().numpy(), out[0])
