@@ -12,7 +12,7 @@
 //   4. ta_shift: the aligned degraded row a[n] = deg[n + D] (0 <= n + D < L_row), else 0.
 // Delay D > 0: the degraded row lags the clean one, deg[n] ~ ref[n - D].
 // Utterance mode (fsem_time_align_utt_f32, P.862 sections 10.3-10.5 as restated in the oracle):
-//   5. ta_utterances: the reference's utterances (speech runs >= 16 ms joined across gaps < 200 ms, at
+//   5. ta_utterances (a wave per row): the reference's utterances (speech runs >= 16 ms joined across gaps < 200 ms, at
 //      least 200 ms long, at most 16), the regions they own (boundaries in the gaps' middles) and
 //      the regions' 5120-sample pieces;
 //   6. ta_crude_utt: each utterance's envelope lag over its search window (+-300 ms around it),
@@ -354,39 +354,39 @@ __global__ void __launch_bounds__(256) ta_shift(const float *__restrict__ deg, i
 }
 
 // ---------------------------------------------------------------- stage 5: utterances
-// One thread per row: a sequential pass over the reference envelope (speech runs of MINSPEECH
-// frames or more, joined across gaps < JOIN frames, kept from MINUTT frames, at most MAXU: later
-// ones join the last), then the
-// regions (boundary: the middle of the gap, in whole frames) and their pieces.  No utterance:
-// one covering the row (its crude window: every frame).
+// One wave per row: the reference envelope 64 frames at a time (one coalesced load, a ballot of
+// the speech frames), the runs of each block walked with bit scans in wave-uniform (scalar)
+// code -- speech runs of MINSPEECH frames or more, joined across gaps < JOIN frames, kept from
+// MINUTT frames, at most MAXU (later ones join the last); then the regions (boundary: the
+// middle of the gap, in whole frames) and their pieces.  No utterance: one covering the row
+// (its crude window: every frame).
 __global__ void __launch_bounds__(64) ta_utterances(int64_t B, int64_t L, const int32_t *__restrict__ lengths,
                                                     const float *__restrict__ E, int64_t nfr_cap,
                                                     int *__restrict__ nutt, int *__restrict__ utt,
                                                     int *__restrict__ reg, int *__restrict__ cs) {
-  const int64_t b = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  __shared__ int us[2 * MAXU];
+  const int64_t b = blockIdx.x + (int64_t)blockIdx.y * 65535;
   if (b >= B) return;
+  const int lane = threadIdx.x;
   const int64_t Lr = row_len(lengths, b, L);
   const int nfr = (int)(Lr / FRAME);
   const float *env = E + b * nfr_cap;
-  int *us = utt + b * (2 * MAXU);
-  int n = 0, s0 = -1, e0 = -1, rs = -1;  // joined run [s0, e0), raw run from rs
+  int n = 0, s0 = -1, e0 = -1, rs = -1;  // utterances, joined run [s0, e0), open raw run from rs
   auto flush = [&]() {
     if (s0 >= 0 && e0 - s0 >= MINUTT) {
       if (n < MAXU) {
-        us[2 * n] = s0;
-        us[2 * n + 1] = e0;
+        if (lane == 0) {
+          us[2 * n] = s0;
+          us[2 * n + 1] = e0;
+        }
         ++n;
-      } else {
+      } else if (lane == 0) {
         us[2 * (MAXU - 1) + 1] = e0;
       }
     }
   };
-  for (int k = 0; k <= nfr; ++k) {
-    if (k < nfr && env[k] > 0.f) {
-      if (rs < 0) rs = k;
-      continue;
-    }
-    if (rs >= 0 && k - rs >= MINSPEECH) {  // the raw run [rs, k) counts
+  auto close_run = [&](int k) {  // the raw run [rs, k) ends
+    if (k - rs >= MINSPEECH) {
       if (s0 >= 0 && rs - e0 < JOIN) {
         e0 = k;
       } else {
@@ -396,21 +396,47 @@ __global__ void __launch_bounds__(64) ta_utterances(int64_t B, int64_t L, const 
       }
     }
     rs = -1;
+  };
+  for (int k0 = 0; k0 < nfr; k0 += 64) {
+    const int k = k0 + lane;
+    const uint64_t m = __ballot(k < nfr && env[k] > 0.f);
+    int pos = 0;
+    while (pos < 64) {
+      if (rs >= 0) {
+        const uint64_t z = ~m >> pos;  // the open run ends at the next inactive frame
+        if (z == 0) break;             // ... in a later block
+        pos += __builtin_ctzll(z);
+        close_run(k0 + pos);
+      } else {
+        const uint64_t o = m >> pos;
+        if (o == 0) break;
+        pos += __builtin_ctzll(o);
+        rs = k0 + pos;
+      }
+    }
   }
+  if (rs >= 0) close_run(nfr);
   flush();
   if (n == 0) {
-    us[0] = 0;
-    us[1] = nfr;
+    if (lane == 0) {
+      us[0] = 0;
+      us[1] = nfr;
+    }
     n = 1;
   }
-  nutt[b] = n;
-  int *rg = reg + b * (MAXU + 1);
-  int *c = cs + b * (MAXU + 1);
-  rg[0] = 0;
-  for (int u = 1; u < n; ++u) rg[u] = FRAME * ((us[2 * u - 1] + us[2 * u]) / 2);
-  rg[n] = (int)Lr;
-  c[0] = 0;
-  for (int u = 0; u < n; ++u) c[u + 1] = c[u] + std::max(1, (rg[u + 1] - rg[u] + CS - 1) / CS);
+  __syncthreads();
+  if (lane == 0) {
+    int *uo = utt + b * (2 * MAXU);
+    for (int i = 0; i < 2 * n; ++i) uo[i] = us[i];
+    nutt[b] = n;
+    int *rg = reg + b * (MAXU + 1);
+    int *c = cs + b * (MAXU + 1);
+    rg[0] = 0;
+    for (int u = 1; u < n; ++u) rg[u] = FRAME * ((us[2 * u - 1] + us[2 * u]) / 2);
+    rg[n] = (int)Lr;
+    c[0] = 0;
+    for (int u = 0; u < n; ++u) c[u + 1] = c[u] + std::max(1, (rg[u + 1] - rg[u] + CS - 1) / CS);
+  }
 }
 
 // First-maximum argmax over a 256-thread workgroup: (v, j) with v > 0, or (0, INT32_MAX).
@@ -786,8 +812,7 @@ extern "C" int fsem_time_align_utt_f32(const float *ref, const float *deg, int64
   FSEM_CHECK_LAUNCH();
   align::ta_crude<<<xy(batch), 256, 0, st>>>(batch, length, lengths, w.E, nfr_cap, max_frames, w.crude);
   FSEM_CHECK_LAUNCH();
-  const unsigned rb = (unsigned)((batch + 63) / 64);
-  align::ta_utterances<<<rb, 64, 0, st>>>(batch, length, lengths, w.E, nfr_cap, w.nutt, w.utt, w.reg, w.cs);
+  align::ta_utterances<<<xy(batch), 64, 0, st>>>(batch, length, lengths, w.E, nfr_cap, w.nutt, w.utt, w.reg, w.cs);
   FSEM_CHECK_LAUNCH();
   {
     dim3 grid = yz(batch);
@@ -805,7 +830,8 @@ extern "C" int fsem_time_align_utt_f32(const float *ref, const float *deg, int64
     align::ta_pick_utt<<<grid, 256, 0, st>>>(batch, w.nutt, w.cs, w.ucrude, (int)nsl, w.part, w.useg);
     FSEM_CHECK_LAUNCH();
   }
-  align::ta_segments<<<rb, 64, 0, st>>>(batch, length, lengths, w.nutt, w.reg, w.useg, ns, ss, sd, dl);
+  align::ta_segments<<<(unsigned)((batch + 63) / 64), 64, 0, st>>>(batch, length, lengths, w.nutt, w.reg, w.useg, ns,
+                                                                 ss, sd, dl);
   FSEM_CHECK_LAUNCH();
   if (deg_aligned) {
     dim3 grid = yz(batch);
