@@ -215,6 +215,11 @@ def kernel_roofline(clean, noisy, reps, joint, config_batch=None):
         sims = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
         out["valu_issue"] = {"instructions_per_launch": n, "frac": round(n * 2 / (sims * 2.4e9 * ms * 1e-3), 4),
                              "source": src}
+    occ = pmc_counter(name, "waves_per_simd", B, L, as_float=True)
+    if occ:
+        # achieved occupancy: mean resident waves per SIMD over the launch (tools/pmc_summary.py:
+        # 4 x SQ_WAVE_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)); 2 is this kernel's limit
+        out["occupancy"] = {"waves_per_simd": round(occ[0], 3), "limit": 2, "source": occ[1]}
     return out
 
 
@@ -230,7 +235,7 @@ def _pmc_meta_ok(d: dict, rows: int, L: int) -> bool:
     return (m.get("rows_per_launch"), m.get("length")) == (rows, L)
 
 
-def pmc_counter(kernel, counter: str, B: int, L: int):
+def pmc_counter(kernel, counter: str, B: int, L: int, as_float: bool = False):
     """(value per launch, source) of one counter of `kernel` (a name suffix, or a tuple of them)
     from the newest committed PMC summary recorded at B rows x L samples per launch."""
     import glob
@@ -249,7 +254,8 @@ def pmc_counter(kernel, counter: str, B: int, L: int):
             continue
         key = next((k for k in d if k.endswith(kernel)), None)
         if key and counter in d[key] and _pmc_meta_ok(d, B, L):
-            best = (int(d[key][counter]), os.path.relpath(f, HERE))
+            v = d[key][counter]
+            best = (float(v) if as_float else int(v), os.path.relpath(f, HERE))
     return best
 
 
