@@ -310,9 +310,12 @@ __device__ __forceinline__ uint32_t dpp_u(uint32_t v) {
 __device__ __forceinline__ uint32_t peak_exponents(float c0, float c1, float c2, float c3, float d0, float d1,
                                                    float d2, float d3) {
   typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-  // exponent field of the larger magnitude (integer max of |x|'s bits: same order as magnitude)
-  auto mx = [](float a, float b) { return max(__float_as_uint(a) & 0x7fffffffu, __float_as_uint(b) & 0x7fffffffu); };
-  const uint32_t mc = max(mx(c0, c1), mx(c2, c3)), md = max(mx(d0, d1), mx(d2, d3));
+  // exponent field of the largest magnitude: a float max over |x| (abs source modifiers, max3)
+  auto mx4 = [](float a, float b, float c, float d) {
+    return __float_as_uint(__builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(a), __builtin_fabsf(b)),
+                                           __builtin_fmaxf(__builtin_fabsf(c), __builtin_fabsf(d))));
+  };
+  const uint32_t mc = mx4(c0, c1, c2, c3), md = mx4(d0, d1, d2, d3);
   uint32_t e = ((mc >> 7) & 0xffff0000u) | (md >> 23);
   auto pmax = [](uint32_t x, uint32_t y) {
     return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(us2, x), __builtin_bit_cast(us2, y)));
