@@ -470,9 +470,15 @@ __global__ void __launch_bounds__(64 * TOB_WAVES)
         mr = v[(8 - r) & 7].r;
         mi = v[(8 - r) & 7].i;
       }
-      const float zr = v[r].r, zi = v[r].i;
-      pa[r] = fmaf(zr + mr, zr + mr, (zi - mi) * (zi - mi));  // explicit: no contraction choice
-      pb[r] = fmaf(zi + mi, zi + mi, (zr - mr) * (zr - mr));
+      // (pa, pb) = (|zr + mr|^2 + (zi - mi)^2, |zi + mi|^2 + (zr - mr)^2) in packed FP32:
+      // the same per-element operations as the scalar form, half the instructions
+      typedef float f2v __attribute__((ext_vector_type(2)));
+      const f2v z = {v[r].r, v[r].i}, m = {mr, mi};
+      const f2v sm = z + m;
+      const f2v df = z.yx - m.yx;  // (zi - mi, zr - mr)
+      const f2v pp = __builtin_elementwise_fma(sm, sm, df * df);
+      pa[r] = pp.x;
+      pb[r] = pp.y;
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -484,9 +490,9 @@ __global__ void __launch_bounds__(64 * TOB_WAVES)
       // band sums: one <=9-bin piece per lane (lanes of piece set 0: frame a, set 1: frame b),
       // segmented shuffle reduction per band
       const float *ps = pbuf + 256 * pc_sig;
-      float acc = 0.f;
+      float acc = (pc_lo < pc_hi) ? ps[pc_lo] : 0.f;
 #pragma unroll
-      for (int i = 0; i < 9; ++i) {  // unconditional reads (inside the frame's 256 powers), masked adds
+      for (int i = 1; i < 9; ++i) {  // unconditional reads (inside the frame's 256 powers), masked adds
         const float x = ps[pc_lo + i];
         acc += (pc_lo + i < pc_hi) ? x : 0.f;
       }
