@@ -380,42 +380,46 @@ __device__ __forceinline__ void bp_step(float x, float p[5], float z[NS], float 
   }
 }
 
-// Packed steady state of the skewed cascade (sections 1-2 and 3-4 as float2 pairs: one
+// Packed steady state of the skewed cascade (sections 1-4 as two float2 pairs: one
 // v_pk_add_f32 and two v_pk_fma_f32 per pair instead of three scalar instructions per section;
 // section 0 and the pre-emphasis stay scalar).  Per element the same operations in the same
 // order as bp_step<0, 4> + pre_step, so the outputs are bitwise those of the scalar form.
+// The pairs are sections (1, 3) and (2, 4): the skewed cascade's next inputs are then (y0, y2)
+// and (y1, y3) = the (1, 3) outputs themselves, so only y2 moves between register pairs (pairs
+// (1, 2), (3, 4) needed three moves per sample; 182 vs 195 VALU per 12 samples, 7.172 vs 7.199
+// ms per joint call, profiles/r4_fa/).
 typedef float pf2 __attribute__((ext_vector_type(2)));
 struct Pk {
-  pf2 za12, zb12, za34, zb34;  // (z[2], z[4]), (z[3], z[5]), (z[6], z[8]), (z[7], z[9])
-  pf2 p12, p34;                // section inputs (p[1], p[2]), (p[3], p[4])
+  pf2 zaA, zbA, zaB, zbB;  // A = sections (1, 3): (z[2], z[6]), (z[3], z[7]); B = (2, 4): (z[4], z[8]), (z[5], z[9])
+  pf2 pA, pB;              // section inputs (p[1], p[3]), (p[2], p[4])
 };
 __device__ __forceinline__ void pk_load(Pk &q, const float z[NS], const float p[5]) {
-  q.za12 = (pf2){z[2], z[4]};
-  q.zb12 = (pf2){z[3], z[5]};
-  q.za34 = (pf2){z[6], z[8]};
-  q.zb34 = (pf2){z[7], z[9]};
-  q.p12 = (pf2){p[1], p[2]};
-  q.p34 = (pf2){p[3], p[4]};
+  q.zaA = (pf2){z[2], z[6]};
+  q.zbA = (pf2){z[3], z[7]};
+  q.zaB = (pf2){z[4], z[8]};
+  q.zbB = (pf2){z[5], z[9]};
+  q.pA = (pf2){p[1], p[3]};
+  q.pB = (pf2){p[2], p[4]};
 }
 __device__ __forceinline__ void pk_store(const Pk &q, float z[NS], float p[5]) {
-  z[2] = q.za12.x; z[4] = q.za12.y; z[3] = q.zb12.x; z[5] = q.zb12.y;
-  z[6] = q.za34.x; z[8] = q.za34.y; z[7] = q.zb34.x; z[9] = q.zb34.y;
-  p[1] = q.p12.x; p[2] = q.p12.y; p[3] = q.p34.x; p[4] = q.p34.y;
+  z[2] = q.zaA.x; z[6] = q.zaA.y; z[3] = q.zbA.x; z[7] = q.zbA.y;
+  z[4] = q.zaB.x; z[8] = q.zaB.y; z[5] = q.zbB.x; z[9] = q.zbB.y;
+  p[1] = q.pA.x; p[3] = q.pA.y; p[2] = q.pB.x; p[4] = q.pB.y;
 }
 // one step: sections 4..1 on their (older) samples, section 0 on x; section 4's output to acc
 __device__ __forceinline__ void pk_step(float x, Pk &q, float z[NS], float &acc) {
-  const pf2 na0_34 = (pf2){-kBpSecA[3][0], -kBpSecA[4][0]}, na1_34 = (pf2){-kBpSecA[3][1], -kBpSecA[4][1]};
-  const pf2 na0_12 = (pf2){-kBpSecA[1][0], -kBpSecA[2][0]}, na1_12 = (pf2){-kBpSecA[1][1], -kBpSecA[2][1]};
-  const pf2 y34 = q.p34 + q.za34;
-  q.za34 = __builtin_elementwise_fma(na0_34, y34, q.zb34);
-  q.zb34 = __builtin_elementwise_fma(na1_34, y34, -q.p34);
-  acc = fmaf(y34.y, y34.y, acc);
-  const pf2 y12 = q.p12 + q.za12;
-  q.za12 = __builtin_elementwise_fma(na0_12, y12, q.zb12);
-  q.zb12 = __builtin_elementwise_fma(na1_12, y12, -q.p12);
+  const pf2 na0_B = (pf2){-kBpSecA[2][0], -kBpSecA[4][0]}, na1_B = (pf2){-kBpSecA[2][1], -kBpSecA[4][1]};
+  const pf2 na0_A = (pf2){-kBpSecA[1][0], -kBpSecA[3][0]}, na1_A = (pf2){-kBpSecA[1][1], -kBpSecA[3][1]};
+  const pf2 yB = q.pB + q.zaB;  // (y2, y4)
+  q.zaB = __builtin_elementwise_fma(na0_B, yB, q.zbB);
+  q.zbB = __builtin_elementwise_fma(na1_B, yB, -q.pB);
+  acc = fmaf(yB.y, yB.y, acc);
+  const pf2 yA = q.pA + q.zaA;  // (y1, y3)
+  q.zaA = __builtin_elementwise_fma(na0_A, yA, q.zbA);
+  q.zbA = __builtin_elementwise_fma(na1_A, yA, -q.pA);
   const float y0 = bp_section(0, x, z);
-  q.p12 = (pf2){y0, y12.x};
-  q.p34 = (pf2){y12.y, y34.x};
+  q.pA = (pf2){y0, yB.x};
+  q.pB = yA;
 }
 __device__ __forceinline__ void skew_group_pk(float4 *__restrict__ w4, int q4, Pk &q, float z[NS], float &acc,
                                               float &h1, float &h2) {
@@ -916,10 +920,15 @@ __global__ void __launch_bounds__(PT, 2)
               mr = v[(8 - r) & 7].r;
               mi = v[(8 - r) & 7].i;
             }
-            const float zr = v[r].r, zi = v[r].i;
-            // 4 |Z_a|^2, 4 |Z_b|^2: the 1/4 is folded into the Bark weights (bcor)
-            pa[h][r] = fmaf(zr + mr, zr + mr, (zi - mi) * (zi - mi));  // explicit: no contraction choice
-            pb[h][r] = fmaf(zi + mi, zi + mi, (zr - mr) * (zr - mr));
+            // 4 |Z_a|^2, 4 |Z_b|^2 (the 1/4 is folded into the Bark weights, bcor) in packed FP32:
+            // (|zr + mr|^2 + (zi - mi)^2, |zi + mi|^2 + (zr - mr)^2), the scalar form's operations
+            typedef float f2v __attribute__((ext_vector_type(2)));
+            const f2v z = {v[r].r, v[r].i}, m = {mr, mi};
+            const f2v sm = z + m;
+            const f2v df = z.yx - m.yx;
+            const f2v pp = __builtin_elementwise_fma(sm, sm, df * df);
+            pa[h][r] = pp.x;
+            pb[h][r] = pp.y;
           }
           if (lane == 0) {  // spec[:, :, 0] = 0 (PESQ.py:136)
             pa[h][0] = 0.f;
