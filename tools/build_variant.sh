@@ -1,7 +1,8 @@
 #!/bin/bash
 # Build libfsem from a source tree into fast_speech_enhancement_metrics_amd/lib/var/NAME.so for
-# A/B runs (tools/ab_bench.sh).  Usage: bash tools/build_variant.sh NAME [GIT_REV]
-# Without GIT_REV the working tree is built; with it, that commit's csrc/include.
+# A/B runs (tools/ab_joint.py).  Usage: bash tools/build_variant.sh NAME [GIT_REV]
+# Without GIT_REV the working tree is built; with it, that commit's csrc/include.  Per-source
+# flags as _build.SOURCE_FLAGS (stoi.hip: the max-ilp scheduler); EXTRA applies to every source.
 set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
 NAME=$1
@@ -14,7 +15,14 @@ if [ -n "$REV" ]; then
   git -C "$R" archive "$REV" fast_speech_enhancement_metrics_amd/csrc include | tar x -C "$SRC"
 fi
 C=$SRC/fast_speech_enhancement_metrics_amd/csrc
-/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -shared -fPIC -Wno-unused-result ${EXTRA:-} \
-  -o "$OUT/$NAME.so" "$C/pesq.hip" "$C/stoi.hip" "$C/resample.hip" $([ -f "$C/align.hip" ] && echo "$C/align.hip")
+T=$(mktemp -d)
+for f in pesq stoi resample align; do
+  [ -f "$C/$f.hip" ] || continue
+  FL=""
+  [ "$f" = "stoi" ] && FL="-mllvm -amdgpu-sched-strategy=max-ilp"
+  /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wno-unused-result $FL ${EXTRA:-} -c -o "$T/$f.o" "$C/$f.hip"
+done
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o "$OUT/$NAME.so" "$T"/*.o
+rm -rf "$T"
 [ -n "$REV" ] && rm -rf "$SRC"
 echo "$OUT/$NAME.so"
