@@ -59,6 +59,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=5)
     ap.add_argument("--separate", action="store_true", help="two API calls (PESQ, STOI) instead of the joint entry")
+    ap.add_argument("--device-list", default=None,
+                    help="with --single-process: explicit device indices, e.g. 0,0 (repeats allowed: "
+                         "several streams on one device -- the 1-GPU rehearsal of the fan-out path)")
     ap.add_argument("--single-process", action="store_true",
                     help="with --gpus N: ONE process drives the N devices (devices=N on the metric, "
                          "multidevice.py) on a batch of N x --batch rows held by device 0 -- the timed "
@@ -465,10 +468,11 @@ def run_single_process(args):
     its own stream, and the scores come back to device 0 (multidevice.py)."""
     from fast_speech_enhancement_metrics_amd import PESQ_STOI
     from fast_speech_enhancement_metrics_amd.synthetic import speech_like_pairs
-    n = args.gpus
+    devices = [int(x) for x in args.device_list.split(",")] if args.device_list else list(range(args.gpus))
+    n = len(devices)
     visible = torch.cuda.device_count()
-    if n > visible:
-        print(f"bench.py: --gpus {n} but only {visible} HIP device(s) are visible", file=sys.stderr)
+    if max(devices) >= visible:
+        print(f"bench.py: devices {devices} but only {visible} HIP device(s) are visible", file=sys.stderr)
         sys.exit(2)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -480,7 +484,7 @@ def run_single_process(args):
         ns.append(x)
     clean, noisy = torch.cat(cs), torch.cat(ns)
     del cs, ns
-    metric = PESQ_STOI(16000, use_gpu=True, devices=n)
+    metric = PESQ_STOI(16000, use_gpu=True, devices=[f"cuda:{d}" for d in devices])
 
     def step():
         return metric(clean, noisy)
@@ -488,13 +492,15 @@ def run_single_process(args):
     dt = _timed(step, args, dev, False)
     print(json.dumps({
         "metric": METRIC + " (one process, devices=N)", "value": round(B * args.steps / dt, 2),
-        "unit": "utterances/s", "n_gpus": n, "steps": args.steps, "warmup": args.warmup,
+        "unit": "utterances/s", "n_gpus": len(set(devices)), "devices": devices, "steps": args.steps,
+        "warmup": args.warmup,
         "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32", "data": "synthetic speech-like pairs, the whole batch on device 0",
         "config": {"workload": "PESQ_STOI(16000, use_gpu=True, devices=N)(c, n) -> list of dicts, including the "
                                "peer copies of N-1 shards from device 0", "batch_per_gpu": args.batch,
                    "global_batch": B, "length": L, "sample_rate": 16000,
-                   "parallelism": f"{n} devices from one process (multidevice.py)"}}), flush=True)
+                   "parallelism": f"{n} shards on devices {devices} from one process (multidevice.py)"}}),
+          flush=True)
 
 
 def main():
