@@ -19,10 +19,13 @@ LIBDIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIBDIR, "libfsem.so")
 STAMP_LIB = os.path.join(LIBDIR, "libfsem_stamps.so")  # diagnostic build (tools/stamps.py)
 SOURCES = ["pesq.hip", "stoi.hip", "resample.hip", "align.hip"]
-# per-source code-generation flags: the STOI kernels are scheduled for ILP (gfx950's max-ilp
-# machine scheduler: 7.167 vs 7.198 ms per joint call, bitwise equal, profiles/r4_sc/); the
-# PESQ front end keeps the default, under which it does not spill (max-ilp: 476 SGPR spills)
-SOURCE_FLAGS = {"stoi.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]}
+# per-source code-generation flags: the STOI kernels and the resamplers are scheduled for ILP
+# (gfx950's max-ilp machine scheduler: joint call 7.167 vs 7.198 ms, profiles/r4_sc/; config 5
+# 224.0k vs 221.3k utt/s, profiles/r4_fl/; bitwise equal); the PESQ front end keeps the
+# default, under which it does not spill (max-ilp: 476 SGPR spills), and so does the time
+# alignment (max-ilp: 19.68 vs 19.49 ms per 4096-row aligned PESQ step)
+_ILP = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
+SOURCE_FLAGS = {"stoi.hip": _ILP, "resample.hip": _ILP}
 HEADERS = ["fsem_common.h", "fsem_fft.h", "fsem_internal.h", "fsem_resample.h", "fsem_tables.inc"]
 ARCH = os.environ.get("FSEM_OFFLOAD_ARCH", "gfx950")
 # the drop-in call's list-of-dicts builder (host C, CPython API; csrc/score_list.c)

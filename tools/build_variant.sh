@@ -19,7 +19,7 @@ T=$(mktemp -d)
 for f in pesq stoi resample align; do
   [ -f "$C/$f.hip" ] || continue
   FL=""
-  [ "$f" = "stoi" ] && FL="-mllvm -amdgpu-sched-strategy=max-ilp"
+  { [ "$f" = "stoi" ] || [ "$f" = "resample" ]; } && FL="-mllvm -amdgpu-sched-strategy=max-ilp"
   /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wno-unused-result $FL ${EXTRA:-} -c -o "$T/$f.o" "$C/$f.hip"
 done
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o "$OUT/$NAME.so" "$T"/*.o
