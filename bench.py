@@ -164,7 +164,7 @@ def kernel_roofline(clean, noisy, reps, joint, config_batch=None):
     """HIP-event timing of the dominant kernel -- pesq_front, launched alone through its stage
     entry (fsem_pesq_front_y10_f32 for the joint path, fsem_pesq_front_f32 otherwise) -- on the
     stream it is launched on, over the rows one engine call of the step processes (the drop-in
-    call's chunk: 2048 of the 4096 rows); achieved = algorithmic bytes per launch / avg duration.
+    call's rows per engine call, joint.chunk_bounds: all 4096); achieved = algorithmic bytes per launch / avg duration.
     `config_batch`: the bench configuration's batch (the PMC summaries are recorded at it)."""
     from fast_speech_enhancement_metrics_amd import _native
     lib = _native.load()

@@ -309,4 +309,8 @@ class PESQ(BaseMetric):
         assert clean_speech is not None
         with torch.inference_mode():
             mos = self.scores(clean_speech, denoised_speech, lengths, sample_rate=self.EXPECTED_SAMPLING_RATE)
-            return _native.score_list(mos.reshape(1, -1).cpu(), ("PESQ",))
+            if not mos.is_cuda:
+                return _native.score_list(mos.reshape(1, -1), ("PESQ",))
+            res = _native.score_list_alloc(mos.numel(), ("PESQ",))  # while the GPU computes
+            _native.score_list_fill(res, 0, mos.reshape(1, -1).cpu(), ("PESQ",))
+            return res

@@ -128,6 +128,41 @@ def score_list(scores, keys: tuple) -> list:
     return mod.score_list(scores, keys)
 
 
+def score_list_alloc(n: int, keys: tuple) -> list:
+    """The drop-in call's result list before its scores are known: n dicts over `keys`, NaN
+    values -- built while the GPU computes; score_list_fill writes the scores into them."""
+    mod = _score_list_mod
+    if mod is None:
+        mod = _load_score_list()
+    if mod is False:
+        score_list_py(_np_empty(len(keys), 0), keys)  # the same argument checks
+        return [dict.fromkeys(keys, float("nan")) for _ in range(n)]
+    return mod.score_list_alloc(n, keys)
+
+
+def score_list_fill(lst: list, offset: int, scores, keys: tuple) -> None:
+    """lst[offset + b][keys[k]] = scores[k][b] for the [K, B] host scores (numpy or a CPU tensor):
+    the same dicts and values as score_list(scores, keys) at lst[offset:offset + B]."""
+    mod = _score_list_mod
+    if mod is None:
+        mod = _load_score_list()
+    if isinstance(scores, torch.Tensor):
+        scores = scores.detach().cpu().contiguous().numpy()
+    if mod is False:
+        rows = score_list_py(scores, keys)
+        if offset < 0 or offset + len(rows) > len(lst):
+            raise IndexError("score_list_fill: rows past the list's end")
+        for b, row in enumerate(rows):
+            lst[offset + b].update(row)
+        return
+    mod.score_list_fill(lst, offset, scores, keys)
+
+
+def _np_empty(k: int, n: int):
+    import numpy as np
+    return np.empty((k, n), dtype=np.float32)
+
+
 class NativeError(RuntimeError):
     pass
 

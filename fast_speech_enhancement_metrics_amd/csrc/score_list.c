@@ -13,38 +13,63 @@
  * never materialises the K intermediate lists.  Optional: where it cannot be built or loaded
  * (no C compiler or Python headers, a read-only package directory), _native.score_list falls
  * back to the Python form with the same result.
+ *
+ * Two-phase form for the GPU path: score_list_alloc(B, keys) builds the B dicts with fresh float
+ * objects while the GPU computes (nothing is known yet but the shape), and
+ * score_list_fill(lst, offset, scores, keys) writes the values into them once a chunk's scores
+ * reach the host -- a few ns per dict instead of ~100, so the list no longer trails the GPU.
+ * The floats are private until the list is returned (created here, referenced once, by their
+ * dict), so setting their value in place is the same as creating them with it, as a fresh tuple
+ * is filled with PyTuple_SET_ITEM; any other object found in a dict (a list the caller touched)
+ * is replaced through PyDict_SetItem instead.
  */
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
 
-static PyObject *score_list(PyObject *self, PyObject *args) {
-  (void)self;
-  PyObject *buf_obj, *keys;
-  if (!PyArg_ParseTuple(args, "OO!", &buf_obj, &PyTuple_Type, &keys)) return NULL;
+/* keys: a non-empty tuple of str (hashes cached once); returns K or -1 with an exception set */
+static Py_ssize_t check_keys(PyObject *keys) {
   const Py_ssize_t K = PyTuple_GET_SIZE(keys);
   if (K <= 0) {
     PyErr_SetString(PyExc_ValueError, "score_list: keys must be a non-empty tuple");
-    return NULL;
+    return -1;
   }
   for (Py_ssize_t k = 0; k < K; ++k) {
     PyObject *key = PyTuple_GET_ITEM(keys, k);
     if (!PyUnicode_Check(key)) {
       PyErr_SetString(PyExc_TypeError, "score_list: keys must be str");
-      return NULL;
+      return -1;
     }
-    if (PyObject_Hash(key) == -1) return NULL; /* cache the hash once */
+    if (PyObject_Hash(key) == -1) return -1; /* cache the hash once */
   }
-  Py_buffer view;
-  if (PyObject_GetBuffer(buf_obj, &view, PyBUF_C_CONTIGUOUS | PyBUF_FORMAT) != 0) return NULL;
-  PyObject *out = NULL;
-  const char *fmt = view.format ? view.format : "";
+  return K;
+}
+
+/* the K x B float32 / float64 scores of buf_obj (view released by the caller on success);
+ * returns B or -1 with an exception set */
+static Py_ssize_t get_scores(PyObject *buf_obj, Py_ssize_t K, Py_buffer *view, int *f64) {
+  if (PyObject_GetBuffer(buf_obj, view, PyBUF_C_CONTIGUOUS | PyBUF_FORMAT) != 0) return -1;
+  const char *fmt = view->format ? view->format : "";
   if (*fmt == '<' || *fmt == '=' || *fmt == '@') ++fmt;
-  const int f64 = fmt[0] == 'd' && fmt[1] == 0 && view.itemsize == 8;
-  if (!(f64 || (fmt[0] == 'f' && fmt[1] == 0 && view.itemsize == 4)) || view.len % (K * view.itemsize) != 0) {
+  *f64 = fmt[0] == 'd' && fmt[1] == 0 && view->itemsize == 8;
+  if (!(*f64 || (fmt[0] == 'f' && fmt[1] == 0 && view->itemsize == 4)) || view->len % (K * view->itemsize) != 0) {
     PyErr_SetString(PyExc_TypeError, "score_list: scores must be a contiguous float32 / float64 buffer of K x B values");
-    goto done;
+    PyBuffer_Release(view);
+    return -1;
   }
-  const Py_ssize_t B = view.len / (K * view.itemsize);
+  return view->len / (K * view->itemsize);
+}
+
+static PyObject *score_list(PyObject *self, PyObject *args) {
+  (void)self;
+  PyObject *buf_obj, *keys;
+  if (!PyArg_ParseTuple(args, "OO!", &buf_obj, &PyTuple_Type, &keys)) return NULL;
+  const Py_ssize_t K = check_keys(keys);
+  if (K < 0) return NULL;
+  Py_buffer view;
+  int f64;
+  const Py_ssize_t B = get_scores(buf_obj, K, &view, &f64);
+  if (B < 0) return NULL;
+  PyObject *out = NULL;
   const float *v = (const float *)view.buf;
   const double *w = (const double *)view.buf;
   out = PyList_New(B);
@@ -69,8 +94,95 @@ done:
   return out;
 }
 
+/* score_list_alloc(B, keys) -> [{keys[0]: nan, ...} x B], every value a fresh float object */
+static PyObject *score_list_alloc(PyObject *self, PyObject *args) {
+  (void)self;
+  Py_ssize_t B;
+  PyObject *keys;
+  if (!PyArg_ParseTuple(args, "nO!", &B, &PyTuple_Type, &keys)) return NULL;
+  if (B < 0) {
+    PyErr_SetString(PyExc_ValueError, "score_list_alloc: negative length");
+    return NULL;
+  }
+  const Py_ssize_t K = check_keys(keys);
+  if (K < 0) return NULL;
+  PyObject *out = PyList_New(B);
+  if (!out) return NULL;
+  for (Py_ssize_t b = 0; b < B; ++b) {
+    PyObject *d = PyDict_New();
+    if (!d) goto fail;
+    PyList_SET_ITEM(out, b, d);
+    for (Py_ssize_t k = 0; k < K; ++k) {
+      PyObject *f = PyFloat_FromDouble(Py_NAN);
+      if (!f) goto fail;
+      const int rc = PyDict_SetItem(d, PyTuple_GET_ITEM(keys, k), f);
+      Py_DECREF(f);
+      if (rc != 0) goto fail;
+    }
+  }
+  return out;
+fail:
+  Py_DECREF(out);
+  return NULL;
+}
+
+/* score_list_fill(lst, offset, scores_KxB, keys): lst[offset + b][keys[k]] = scores[k][b] */
+static PyObject *score_list_fill(PyObject *self, PyObject *args) {
+  (void)self;
+  PyObject *lst, *buf_obj, *keys;
+  Py_ssize_t off;
+  if (!PyArg_ParseTuple(args, "O!nOO!", &PyList_Type, &lst, &off, &buf_obj, &PyTuple_Type, &keys)) return NULL;
+  const Py_ssize_t K = check_keys(keys);
+  if (K < 0) return NULL;
+  Py_buffer view;
+  int f64;
+  const Py_ssize_t B = get_scores(buf_obj, K, &view, &f64);
+  if (B < 0) return NULL;
+  PyObject *ret = NULL;
+  if (off < 0 || off > PyList_GET_SIZE(lst) - B) {
+    PyErr_SetString(PyExc_IndexError, "score_list_fill: rows past the list's end");
+    goto done;
+  }
+  const float *v = (const float *)view.buf;
+  const double *w = (const double *)view.buf;
+  for (Py_ssize_t b = 0; b < B; ++b) {
+    PyObject *d = PyList_GET_ITEM(lst, off + b);
+    if (!PyDict_Check(d)) {
+      PyErr_SetString(PyExc_TypeError, "score_list_fill: list items must be dicts");
+      goto done;
+    }
+    Py_ssize_t pos = 0, k = 0;
+    PyObject *key, *val;
+    int fast = PyDict_CheckExact(d) && PyDict_GET_SIZE(d) == K;
+    /* fast path: the dict as score_list_alloc built it (keys in order, private floats) */
+    while (fast && k < K && PyDict_Next(d, &pos, &key, &val)) {
+      if (key != PyTuple_GET_ITEM(keys, k) || !PyFloat_CheckExact(val) || Py_REFCNT(val) != 1) {
+        fast = 0;
+        break;
+      }
+      ((PyFloatObject *)val)->ob_fval = f64 ? w[k * B + b] : (double)v[k * B + b];
+      ++k;
+    }
+    for (; k < K; ++k) { /* anything else: new floats through the dict API */
+      PyObject *f = PyFloat_FromDouble(f64 ? w[k * B + b] : (double)v[k * B + b]);
+      if (!f) goto done;
+      const int rc = PyDict_SetItem(d, PyTuple_GET_ITEM(keys, k), f);
+      Py_DECREF(f);
+      if (rc != 0) goto done;
+    }
+  }
+  ret = Py_None;
+  Py_INCREF(ret);
+done:
+  PyBuffer_Release(&view);
+  return ret;
+}
+
 static PyMethodDef methods[] = {
     {"score_list", score_list, METH_VARARGS, "score_list(scores_f32_KxB, keys) -> list of dicts"},
+    {"score_list_alloc", score_list_alloc, METH_VARARGS, "score_list_alloc(B, keys) -> list of B dicts (nan values)"},
+    {"score_list_fill", score_list_fill, METH_VARARGS,
+     "score_list_fill(lst, offset, scores_f32_KxB, keys): write the scores into lst[offset:offset+B]"},
     {NULL, NULL, 0, NULL},
 };
 

@@ -99,20 +99,23 @@ class PESQ_STOI(BaseMetric):
         assert clean_speech is not None
         return self._listed(clean_speech, denoised_speech, lengths)[0]
 
-    # Rows per chunk from which the drop-in call pipelines its host work (below); 0 disables it.
-    # Measured at 4096 x 10 s (tools/dropin_cost.py): with the native list builder (0.21 ms per
-    # 4096 dicts) two chunks of 2048 take 8.29 ms per call against 8.39 ms for one (scores alone:
-    # 8.11 ms; profiles/r3_c/dropin.json); chunks of 1024 cost more GPU time than they hide
-    # (8.52 ms).  Batches under two chunks run as one call.
-    pipeline_rows = 2048
+    # Rows per chunk when the drop-in call splits a GPU batch into consecutive engine calls
+    # (below); 0: one call.  The chunks existed to overlap building chunk k's dicts with chunk
+    # k+1's kernels (round 3, profiles/r3_c/dropin.json: 2 x 2048 rows 8.29 ms per call against
+    # 8.39 ms for one).  Since the dicts are built before the scores exist and only filled
+    # afterwards (score_list_alloc / score_list_fill), one call is the faster plan at 4096 x 10 s:
+    # 7.363 ms against 7.428 ms for 2 x 2048 (tools/ab_dropin_chunks.py,
+    # profiles/r4_zz/ab_dropin_fill.txt) -- one kernel tail instead of two.
+    pipeline_rows = 0
 
     def _listed(self, clean_speech, denoised_speech, lengths):
         """(list of dicts, [B, 3] float32 scores on the metric's device) of 16 kHz rows.
 
         On the GPU a large batch is scored in consecutive chunks, all enqueued at once, each
-        followed by an asynchronous copy of its scores into pinned host memory: the dicts of a
-        chunk are built while the GPU computes the next one, so only the last chunk's list
-        building (about 80 ns per utterance) stays outside the GPU time.  Scores are those of
+        followed by an asynchronous copy of its scores into pinned host memory.  The result's dicts
+        are built while the GPU computes (score_list_alloc, ~100 ns per utterance) and each chunk's
+        scores are written into them when its copy lands (score_list_fill, ~15 ns per
+        utterance), so little host work trails the GPU.  Scores are those of
         one call over the whole batch (rows are independent; the PESQ back end's summation order
         depends only on the batch's size class, pesq.hip back_waves)."""
         with torch.inference_mode():
@@ -123,7 +126,11 @@ class PESQ_STOI(BaseMetric):
             if K <= 1:
                 out = torch.stack([t.float() for t in self.scores(clean_speech, denoised_speech, lengths,
                                                                   sample_rate=16000)])
-                res = _native.score_list(out.cpu(), _KEYS)  # the one device -> host copy
+                if out.is_cuda:  # the dicts are built while the GPU computes, then filled
+                    res = _native.score_list_alloc(B, _KEYS)
+                    _native.score_list_fill(res, 0, out.cpu(), _KEYS)  # the one device -> host copy
+                else:
+                    res = _native.score_list(out, _KEYS)
             else:
                 clean = torch.atleast_2d(clean_speech)
                 lens = None if lengths is None else device_lengths(lengths, B, rows.shape[-1], rows.device)
@@ -140,10 +147,10 @@ class PESQ_STOI(BaseMetric):
                     parts.append(part)
                     done.append(ev)
                 out = torch.cat(parts, dim=1)
-                res = []
+                res = _native.score_list_alloc(B, _KEYS)  # while the GPU computes
                 for (lo, hi), ev in zip(bounds, done):
                     ev.synchronize()
-                    res.extend(_native.score_list(pinned[3 * lo:3 * hi].view(3, hi - lo).numpy(), _KEYS))
+                    _native.score_list_fill(res, lo, pinned[3 * lo:3 * hi].view(3, hi - lo).numpy(), _KEYS)
         if all(d["STOI"] != d["STOI"] for d in res):  # as STOI (STOI.py:162-165)
             warnings.warn("Not enough non-silent frames. Please check your sound files", RuntimeWarning, stacklevel=4)
         return res, out.t()

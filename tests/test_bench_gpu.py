@@ -49,9 +49,9 @@ def test_bench_gpus_beyond_visible_fails():
 
 
 def test_bench_rccl_path_one_rank_pipelined():
-    """The driver's multi-GPU launch form (torch.distributed.run, RCCL) with one rank, at a batch
-    where the drop-in call pipelines two 2048-row chunks (joint.py pipeline_rows) and the scores
-    are all-gathered: one JSON line, n_gpus 1."""
+    """The driver's multi-GPU launch form (torch.distributed.run, RCCL) with one rank, at the
+    bench batch (the drop-in call's list plus its [B, 3] scores, all-gathered): one JSON line,
+    n_gpus 1."""
     import socket
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))

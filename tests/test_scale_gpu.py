@@ -60,14 +60,14 @@ def test_bench_config_rows_vs_oracle_and_batch_independence(batch):
 
 
 def test_dropin_call_equals_scores_at_bench_size(batch):
-    """The drop-in call pipelines its host work over chunks (joint.py _listed): its dicts are the
-    one-call scores bitwise, in row order."""
+    """The drop-in call's dicts (built before the scores, filled afterwards; joint.py _listed) are
+    the one-call scores bitwise, in row order -- also with the batch split into chunks."""
     from fast_speech_enhancement_metrics_amd import PESQ_STOI
     c, n = batch
     m = PESQ_STOI(16000, use_gpu=True)
-    assert m.pipeline_rows == 2048  # the default: two chunks at the bench size
+    assert m.pipeline_rows == 0 and m.chunk_bounds(B) == [(0, B)]  # the default: one engine call
     res = m(c, n)
-    m.pipeline_rows = 0
+    m.pipeline_rows = 2048
     assert [d["PESQ"] for d in res] == [d["PESQ"] for d in m(c, n)]
     mos, s, e = (t.cpu().numpy() for t in m.scores(c, n))
     assert len(res) == B

@@ -107,3 +107,57 @@ def test_unbuildable_native_builder_falls_back(monkeypatch):
         got = _native.score_list(np.array([[1.0, 2.0]], np.float32), ("PESQ",))
     assert got == [{"PESQ": 1.0}, {"PESQ": 2.0}]
     assert _native._score_list_mod is False
+
+
+@pytest.fixture(params=["native", "python"])
+def builder(request, monkeypatch):
+    if request.param == "python":
+        monkeypatch.setattr(_native, "_score_list_mod", False)
+    return request.param
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+def test_alloc_fill_matches_score_list(dtype, builder):
+    """The GPU path's two-phase form (dicts built before the scores exist, filled per chunk)
+    returns the list score_list builds: same keys in order, same float values, NaN included."""
+    g = torch.Generator().manual_seed(2)
+    t = torch.randn(3, 300, generator=g, dtype=dtype)
+    t[1, 7] = float("nan")
+    keys = ("PESQ", "STOI", "ESTOI")
+    lst = _native.score_list_alloc(300, keys)
+    assert len(lst) == 300 and all(list(d) == list(keys) and all(math.isnan(v) for v in d.values()) for d in lst)
+    for lo, hi in ((0, 120), (120, 300)):  # chunks, in any order
+        _native.score_list_fill(lst, lo, t[:, lo:hi].contiguous(), keys)
+    want = _py(t, keys)
+    for a, b in zip(lst, want):
+        assert list(a) == list(keys)
+        for k in keys:
+            assert (math.isnan(a[k]) and math.isnan(b[k])) or a[k] == b[k]
+            assert type(a[k]) is float
+    assert _native.score_list_alloc(0, keys) == []
+
+
+def test_fill_leaves_shared_objects_alone(builder):
+    """A float the caller holds is replaced, never written in place; tampered dicts still get
+    every key."""
+    keys = ("STOI", "ESTOI")
+    lst = _native.score_list_alloc(3, keys)
+    held = lst[0]["STOI"]
+    lst[1]["extra"] = 1.0
+    del lst[2]["STOI"]
+    _native.score_list_fill(lst, 0, np.array([[0.5, 0.25, 0.125], [1.0, 2.0, 3.0]], np.float32), keys)
+    assert math.isnan(held)
+    assert lst[0] == {"STOI": 0.5, "ESTOI": 1.0}
+    assert lst[1] == {"STOI": 0.25, "ESTOI": 2.0, "extra": 1.0}
+    assert lst[2] == {"STOI": 0.125, "ESTOI": 3.0}
+
+
+def test_fill_rejects_bad_input(builder):
+    keys = ("PESQ",)
+    lst = _native.score_list_alloc(2, keys)
+    with pytest.raises(IndexError):
+        _native.score_list_fill(lst, 1, np.zeros((1, 2), np.float32), keys)
+    with pytest.raises(TypeError):
+        _native.score_list_fill(lst, 0, np.zeros((1, 2), np.int32), keys)
+    with pytest.raises(ValueError):
+        _native.score_list_alloc(2, ())

@@ -18,8 +18,8 @@ a = ap.parse_args()
 c, n, _ = speech_like_pairs(a.batch, a.length, device="cuda")
 p, s = PESQ(16000, use_gpu=True), STOI(16000, use_gpu=True)
 j = PESQ_STOI(16000, use_gpu=True)
-# the drop-in call as bench.py times it (2048-row engine calls at B = 4096): per-launch counters at
-# the roofline's size (PMC_ROWS in the drivers)
+# the drop-in call as bench.py times it (one 4096-row engine call, joint.chunk_bounds): per-launch
+# counters at the roofline's size (PMC_ROWS in the drivers)
 for _ in range(a.reps):
     if a.joint:
         rp = rs = j(c, n)

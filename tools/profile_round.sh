@@ -15,5 +15,5 @@ bash tools/pmc_lds.sh $TAG --joint > $OUT/pmc_lds_valu.txt || exit 1
 timeout -k 10 300 python bench.py --workload pesq --no-cpu-baseline > $OUT/bench_pesq.json 2> $OUT/bench_pesq.err || exit 1
 timeout -k 10 300 python bench.py --workload c3 --no-cpu-baseline > $OUT/bench_c3.json 2> $OUT/bench_c3.err || exit 1
 timeout -k 10 300 python bench.py --workload c5 --no-cpu-baseline > $OUT/bench_c5.json 2> $OUT/bench_c5.err || exit 1
-PMC_ROWS=2048 python tools/pmc_summary.py $OUT > $OUT/pmc_summary.json || exit 1
+PMC_ROWS=4096 python tools/pmc_summary.py $OUT > $OUT/pmc_summary.json || exit 1
 echo PROFILE_DONE
