@@ -581,26 +581,34 @@ __global__ void __launch_bounds__(SEG_T, 3)
         // correctly rounded sequences: ~1e-7 relative per segment, far inside the tolerance.
         const float alpha = __builtin_amdgcn_sqrtf(s2.x) * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(s2.y) + 1e-9f);
         const f2 sc = {kClip, alpha};  // (x * kClip, alpha * y): one packed multiply
-        float c[NSEG];
-        float syc = 0.f;
+        // the clipped row by frame pairs (c[2u], c[2u + 1]), so its sum, centring and squares are
+        // packed operations too (even / odd partial sums)
+        static_assert(NSEG % 2 == 0, "frame pairs");
+        f2 c[NSEG / 2];
+        f2 syc2 = {0.f, 0.f};
 #pragma unroll
-        for (int t = 0; t < NSEG; ++t) {
-          const f2 q = v[t] * sc;
-          c[t] = fminf(q.y, q.x);
-          syc += c[t];
+        for (int u = 0; u < NSEG / 2; ++u) {
+          const f2 q0 = v[2 * u] * sc, q1 = v[2 * u + 1] * sc;
+          c[u] = (f2){fminf(q0.y, q0.x), fminf(q1.y, q1.x)};
+          syc2 += c[u];
         }
         const f2 mu = s1 * kInvN;
-        const float myc = syc * kInvN;
+        const float myc = (syc2.x + syc2.y) * kInvN;
+        const f2 myc2 = {myc, myc};
         f2 dd = {0.f, 0.f};  // (sum dx^2, sum dy^2)
-        float dcc = 0.f, dxc = 0.f;
+        f2 dcc2 = {0.f, 0.f};
+        float dxc = 0.f;
 #pragma unroll
-        for (int t = 0; t < NSEG; ++t) {
-          const f2 d = v[t] - mu;
-          const float dc = c[t] - myc;
-          dd = __builtin_elementwise_fma(d, d, dd);
-          dcc = fmaf(dc, dc, dcc);
-          dxc = fmaf(d.x, dc, dxc);
+        for (int u = 0; u < NSEG / 2; ++u) {
+          const f2 d0 = v[2 * u] - mu, d1 = v[2 * u + 1] - mu;
+          const f2 dc = c[u] - myc2;
+          dd = __builtin_elementwise_fma(d0, d0, dd);
+          dd = __builtin_elementwise_fma(d1, d1, dd);
+          dcc2 = __builtin_elementwise_fma(dc, dc, dcc2);
+          dxc = fmaf(d0.x, dc.x, dxc);
+          dxc = fmaf(d1.x, dc.y, dxc);
         }
+        const float dcc = dcc2.x + dcc2.y;
         // normalize() (STOI.py:113-119) centres, adds 1e-12 * randn and divides by the norm: in
         // expectation the squared norm gains N * 1e-24 (N = 30 frames) and the noise itself
         // averages out of the correlation.  So 1 / sqrt(||row - mean||^2 + 30e-24): the same

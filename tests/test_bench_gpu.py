@@ -53,15 +53,18 @@ def test_bench_rccl_path_one_rank_pipelined():
     bench batch (the drop-in call's list plus its [B, 3] scores, all-gathered): one JSON line,
     n_gpus 1."""
     import socket
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
-    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
-                          "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(REPO, "bench.py"),
-                          "--gpus", "1", "--batch", "4096", "--length", "16000", "--steps", "2", "--warmup", "1",
-                          "--kernel-reps", "1", "--no-cpu-baseline"],
-                         cwd=REPO, capture_output=True, text=True, timeout=240, env=env)
+    for _ in range(3):  # a fresh port when another process took the probed one (nothing ran yet)
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                              "--master-addr", "127.0.0.1", "--master-port", str(port),
+                              os.path.join(REPO, "bench.py"), "--gpus", "1", "--batch", "4096", "--length", "16000",
+                              "--steps", "2", "--warmup", "1", "--kernel-reps", "1", "--no-cpu-baseline"],
+                             cwd=REPO, capture_output=True, text=True, timeout=240, env=env)
+        if "EADDRINUSE" not in out.stderr:
+            break
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.strip().startswith("{")]
     assert len(lines) == 1, out.stdout
