@@ -206,14 +206,14 @@ class STOI(BaseMetric):
     def _finish(self, stois: torch.Tensor, estois: torch.Tensor) -> list[dict[str, float]]:
         t = torch.stack([stois.float(), estois.float()])
         # on the GPU the dicts are built while it computes, then filled
-        res = _native.score_list_alloc(t.shape[1], ("STOI", "ESTOI")) if t.is_cuda else None
+        res, h = _native.score_list_alloc(t.shape[1], ("STOI", "ESTOI")) if t.is_cuda else (None, None)
         t = t.cpu()
         if bool(torch.isnan(t[0]).all()):  # no utterance has a 30-frame segment (STOI.py:162-165)
             warnings.warn("Not enough non-silent frames. Please check your sound files", RuntimeWarning, stacklevel=3)
             raise TypeError("iteration over a 0-d tensor")
         if res is None:
             return _native.score_list(t, ("STOI", "ESTOI"))
-        _native.score_list_fill(res, 0, t, ("STOI", "ESTOI"))
+        _native.score_list_fill(h, 0, t, ("STOI", "ESTOI"))
         return res
 
     def _resample_cpu(self, x: torch.Tensor, sr: int) -> torch.Tensor:

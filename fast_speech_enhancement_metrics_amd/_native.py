@@ -128,34 +128,40 @@ def score_list(scores, keys: tuple) -> list:
     return mod.score_list(scores, keys)
 
 
-def score_list_alloc(n: int, keys: tuple) -> list:
-    """The drop-in call's result list before its scores are known: n dicts over `keys`, NaN
-    values -- built while the GPU computes; score_list_fill writes the scores into them."""
+def score_list_alloc(n: int, keys: tuple):
+    """The drop-in call's result list before its scores are known: (list of n dicts over `keys`
+    with NaN values, handle) -- built while the GPU computes; score_list_fill(handle, ...)
+    writes the scores into the list."""
     mod = _score_list_mod
     if mod is None:
         mod = _load_score_list()
     if mod is False:
         score_list_py(_np_empty(len(keys), 0), keys)  # the same argument checks
-        return [dict.fromkeys(keys, float("nan")) for _ in range(n)]
+        lst = [dict.fromkeys(keys, float("nan")) for _ in range(n)]
+        return lst, (lst, keys)
     return mod.score_list_alloc(n, keys)
 
 
-def score_list_fill(lst: list, offset: int, scores, keys: tuple) -> None:
-    """lst[offset + b][keys[k]] = scores[k][b] for the [K, B] host scores (numpy or a CPU tensor):
-    the same dicts and values as score_list(scores, keys) at lst[offset:offset + B]."""
+def score_list_fill(handle, offset: int, scores, keys: tuple) -> None:
+    """list[offset + b][keys[k]] = scores[k][b] for the [K, B] host scores (numpy or a CPU tensor)
+    and the list of score_list_alloc's handle: the same dicts and values as
+    score_list(scores, keys) at list[offset:offset + B]."""
     mod = _score_list_mod
     if mod is None:
         mod = _load_score_list()
     if isinstance(scores, torch.Tensor):
         scores = scores.detach().cpu().contiguous().numpy()
     if mod is False:
+        lst, akeys = handle
+        if tuple(keys) != akeys:
+            raise ValueError("score_list_fill: keys differ from the allocation's")
         rows = score_list_py(scores, keys)
         if offset < 0 or offset + len(rows) > len(lst):
             raise IndexError("score_list_fill: rows past the list's end")
         for b, row in enumerate(rows):
             lst[offset + b].update(row)
         return
-    mod.score_list_fill(lst, offset, scores, keys)
+    mod.score_list_fill(handle, offset, scores, keys)
 
 
 def _np_empty(k: int, n: int):

@@ -15,13 +15,14 @@
  * back to the Python form with the same result.
  *
  * Two-phase form for the GPU path: score_list_alloc(B, keys) builds the B dicts with fresh float
- * objects while the GPU computes (nothing is known yet but the shape), and
- * score_list_fill(lst, offset, scores, keys) writes the values into them once a chunk's scores
- * reach the host -- a few ns per dict instead of ~100, so the list no longer trails the GPU.
- * The floats are private until the list is returned (created here, referenced once, by their
- * dict), so setting their value in place is the same as creating them with it, as a fresh tuple
- * is filled with PyTuple_SET_ITEM; any other object found in a dict (a list the caller touched)
- * is replaced through PyDict_SetItem instead.
+ * objects while the GPU computes (nothing is known yet but the shape) and returns them with a
+ * handle holding a reference to every float; score_list_fill(handle, offset, scores, keys)
+ * writes the values into them once a chunk's scores reach the host -- a few ns per dict instead
+ * of ~100, so the list no longer trails the GPU.  The floats are private until the list is
+ * returned (created here, referenced by their dict and the handle only), so setting their value
+ * in place is the same as creating them with it, as a fresh tuple is filled with
+ * PyTuple_SET_ITEM; a float referenced anywhere else (a list the caller touched) is left alone
+ * and its dict gets a new one through PyDict_SetItem.
  */
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
@@ -94,7 +95,27 @@ done:
   return out;
 }
 
-/* score_list_alloc(B, keys) -> [{keys[0]: nan, ...} x B], every value a fresh float object */
+/* The two-phase form's handle: the list and, per row and key, its float object (one extra
+ * reference each, so none can be freed behind the handle's back). */
+typedef struct {
+  PyObject *lst;
+  Py_ssize_t B, K;
+  PyObject **f; /* B x K */
+} Pending;
+
+static void pending_free(PyObject *cap) {
+  Pending *p = (Pending *)PyCapsule_GetPointer(cap, "fsem.score_list");
+  if (!p) return;
+  if (p->f) {
+    for (Py_ssize_t i = 0; i < p->B * p->K; ++i) Py_XDECREF(p->f[i]);
+    PyMem_Free(p->f);
+  }
+  Py_XDECREF(p->lst);
+  PyMem_Free(p);
+}
+
+/* score_list_alloc(B, keys) -> (list, handle): [{keys[0]: nan, ...} x B], every value a fresh
+ * float object, and the handle score_list_fill writes the scores through */
 static PyObject *score_list_alloc(PyObject *self, PyObject *args) {
   (void)self;
   Py_ssize_t B;
@@ -106,68 +127,83 @@ static PyObject *score_list_alloc(PyObject *self, PyObject *args) {
   }
   const Py_ssize_t K = check_keys(keys);
   if (K < 0) return NULL;
-  PyObject *out = PyList_New(B);
-  if (!out) return NULL;
+  Pending *p = (Pending *)PyMem_Calloc(1, sizeof(Pending));
+  if (!p) return PyErr_NoMemory();
+  PyObject *cap = PyCapsule_New(p, "fsem.score_list", pending_free);
+  if (!cap) {
+    PyMem_Free(p);
+    return NULL;
+  }
+  p->f = (PyObject **)PyMem_Calloc((size_t)(B * K) + 1, sizeof(PyObject *));
+  p->lst = PyList_New(B);
+  if (!p->f || !p->lst) {
+    const int oom = !p->f;
+    Py_DECREF(cap); /* frees p */
+    return oom ? PyErr_NoMemory() : NULL;
+  }
+  p->B = B;
+  p->K = K;
   for (Py_ssize_t b = 0; b < B; ++b) {
     PyObject *d = PyDict_New();
     if (!d) goto fail;
-    PyList_SET_ITEM(out, b, d);
+    PyList_SET_ITEM(p->lst, b, d);
     for (Py_ssize_t k = 0; k < K; ++k) {
       PyObject *f = PyFloat_FromDouble(Py_NAN);
       if (!f) goto fail;
-      const int rc = PyDict_SetItem(d, PyTuple_GET_ITEM(keys, k), f);
-      Py_DECREF(f);
-      if (rc != 0) goto fail;
+      p->f[b * K + k] = f; /* the handle's reference */
+      if (PyDict_SetItem(d, PyTuple_GET_ITEM(keys, k), f) != 0) goto fail;
     }
   }
-  return out;
+  return Py_BuildValue("(ON)", p->lst, cap);
 fail:
-  Py_DECREF(out);
+  Py_DECREF(cap);
   return NULL;
 }
 
-/* score_list_fill(lst, offset, scores_KxB, keys): lst[offset + b][keys[k]] = scores[k][b] */
+/* score_list_fill(handle, offset, scores_KxB, keys): lst[offset + b][keys[k]] = scores[k][b] */
 static PyObject *score_list_fill(PyObject *self, PyObject *args) {
   (void)self;
-  PyObject *lst, *buf_obj, *keys;
+  PyObject *cap, *buf_obj, *keys;
   Py_ssize_t off;
-  if (!PyArg_ParseTuple(args, "O!nOO!", &PyList_Type, &lst, &off, &buf_obj, &PyTuple_Type, &keys)) return NULL;
+  if (!PyArg_ParseTuple(args, "OnOO!", &cap, &off, &buf_obj, &PyTuple_Type, &keys)) return NULL;
+  Pending *p = (Pending *)PyCapsule_GetPointer(cap, "fsem.score_list");
+  if (!p) return NULL;
   const Py_ssize_t K = check_keys(keys);
   if (K < 0) return NULL;
+  if (K != p->K) {
+    PyErr_SetString(PyExc_ValueError, "score_list_fill: keys differ from the allocation's");
+    return NULL;
+  }
   Py_buffer view;
   int f64;
   const Py_ssize_t B = get_scores(buf_obj, K, &view, &f64);
   if (B < 0) return NULL;
   PyObject *ret = NULL;
-  if (off < 0 || off > PyList_GET_SIZE(lst) - B) {
+  if (off < 0 || off > p->B - B) {
     PyErr_SetString(PyExc_IndexError, "score_list_fill: rows past the list's end");
     goto done;
   }
   const float *v = (const float *)view.buf;
   const double *w = (const double *)view.buf;
   for (Py_ssize_t b = 0; b < B; ++b) {
-    PyObject *d = PyList_GET_ITEM(lst, off + b);
-    if (!PyDict_Check(d)) {
-      PyErr_SetString(PyExc_TypeError, "score_list_fill: list items must be dicts");
-      goto done;
-    }
-    Py_ssize_t pos = 0, k = 0;
-    PyObject *key, *val;
-    int fast = PyDict_CheckExact(d) && PyDict_GET_SIZE(d) == K;
-    /* fast path: the dict as score_list_alloc built it (keys in order, private floats) */
-    while (fast && k < K && PyDict_Next(d, &pos, &key, &val)) {
-      if (key != PyTuple_GET_ITEM(keys, k) || !PyFloat_CheckExact(val) || Py_REFCNT(val) != 1) {
-        fast = 0;
-        break;
+    for (Py_ssize_t k = 0; k < K; ++k) {
+      const double x = f64 ? w[k * B + b] : (double)v[k * B + b];
+      PyObject *f = p->f[(off + b) * K + k];
+      if (Py_REFCNT(f) == 2) {
+        /* referenced by its dict and the handle only: not yet visible to anyone else */
+        ((PyFloatObject *)f)->ob_fval = x;
+        continue;
       }
-      ((PyFloatObject *)val)->ob_fval = f64 ? w[k * B + b] : (double)v[k * B + b];
-      ++k;
-    }
-    for (; k < K; ++k) { /* anything else: new floats through the dict API */
-      PyObject *f = PyFloat_FromDouble(f64 ? w[k * B + b] : (double)v[k * B + b]);
-      if (!f) goto done;
-      const int rc = PyDict_SetItem(d, PyTuple_GET_ITEM(keys, k), f);
-      Py_DECREF(f);
+      /* replaced or shared since the allocation: a new float through the dict API */
+      PyObject *d = PyList_GET_ITEM(p->lst, off + b);
+      if (!PyDict_Check(d)) {
+        PyErr_SetString(PyExc_TypeError, "score_list_fill: list items must be dicts");
+        goto done;
+      }
+      PyObject *nf = PyFloat_FromDouble(x);
+      if (!nf) goto done;
+      const int rc = PyDict_SetItem(d, PyTuple_GET_ITEM(keys, k), nf);
+      Py_DECREF(nf);
       if (rc != 0) goto done;
     }
   }
@@ -180,9 +216,10 @@ done:
 
 static PyMethodDef methods[] = {
     {"score_list", score_list, METH_VARARGS, "score_list(scores_f32_KxB, keys) -> list of dicts"},
-    {"score_list_alloc", score_list_alloc, METH_VARARGS, "score_list_alloc(B, keys) -> list of B dicts (nan values)"},
+    {"score_list_alloc", score_list_alloc, METH_VARARGS,
+     "score_list_alloc(B, keys) -> (list of B dicts with nan values, handle)"},
     {"score_list_fill", score_list_fill, METH_VARARGS,
-     "score_list_fill(lst, offset, scores_f32_KxB, keys): write the scores into lst[offset:offset+B]"},
+     "score_list_fill(handle, offset, scores_f32_KxB, keys): write the scores into list[offset:offset+B]"},
     {NULL, NULL, 0, NULL},
 };
 

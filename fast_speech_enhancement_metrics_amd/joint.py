@@ -114,7 +114,7 @@ class PESQ_STOI(BaseMetric):
         On the GPU a large batch is scored in consecutive chunks, all enqueued at once, each
         followed by an asynchronous copy of its scores into pinned host memory.  The result's dicts
         are built while the GPU computes (score_list_alloc, ~100 ns per utterance) and each chunk's
-        scores are written into them when its copy lands (score_list_fill, ~15 ns per
+        scores are written into them when its copy lands (score_list_fill, ~10 ns per
         utterance), so little host work trails the GPU.  Scores are those of
         one call over the whole batch (rows are independent; the PESQ back end's summation order
         depends only on the batch's size class, pesq.hip back_waves)."""
@@ -127,8 +127,8 @@ class PESQ_STOI(BaseMetric):
                 out = torch.stack([t.float() for t in self.scores(clean_speech, denoised_speech, lengths,
                                                                   sample_rate=16000)])
                 if out.is_cuda:  # the dicts are built while the GPU computes, then filled
-                    res = _native.score_list_alloc(B, _KEYS)
-                    _native.score_list_fill(res, 0, out.cpu(), _KEYS)  # the one device -> host copy
+                    res, h = _native.score_list_alloc(B, _KEYS)
+                    _native.score_list_fill(h, 0, out.cpu(), _KEYS)  # the one device -> host copy
                 else:
                     res = _native.score_list(out, _KEYS)
             else:
@@ -147,10 +147,10 @@ class PESQ_STOI(BaseMetric):
                     parts.append(part)
                     done.append(ev)
                 out = torch.cat(parts, dim=1)
-                res = _native.score_list_alloc(B, _KEYS)  # while the GPU computes
+                res, h = _native.score_list_alloc(B, _KEYS)  # while the GPU computes
                 for (lo, hi), ev in zip(bounds, done):
                     ev.synchronize()
-                    _native.score_list_fill(res, lo, pinned[3 * lo:3 * hi].view(3, hi - lo).numpy(), _KEYS)
+                    _native.score_list_fill(h, lo, pinned[3 * lo:3 * hi].view(3, hi - lo).numpy(), _KEYS)
         if all(d["STOI"] != d["STOI"] for d in res):  # as STOI (STOI.py:162-165)
             warnings.warn("Not enough non-silent frames. Please check your sound files", RuntimeWarning, stacklevel=4)
         return res, out.t()

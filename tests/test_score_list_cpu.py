@@ -124,40 +124,48 @@ def test_alloc_fill_matches_score_list(dtype, builder):
     t = torch.randn(3, 300, generator=g, dtype=dtype)
     t[1, 7] = float("nan")
     keys = ("PESQ", "STOI", "ESTOI")
-    lst = _native.score_list_alloc(300, keys)
+    lst, h = _native.score_list_alloc(300, keys)
     assert len(lst) == 300 and all(list(d) == list(keys) and all(math.isnan(v) for v in d.values()) for d in lst)
-    for lo, hi in ((0, 120), (120, 300)):  # chunks, in any order
-        _native.score_list_fill(lst, lo, t[:, lo:hi].contiguous(), keys)
+    for lo, hi in ((120, 300), (0, 120)):  # chunks, in any order
+        _native.score_list_fill(h, lo, t[:, lo:hi].contiguous(), keys)
+    del h
     want = _py(t, keys)
     for a, b in zip(lst, want):
         assert list(a) == list(keys)
         for k in keys:
             assert (math.isnan(a[k]) and math.isnan(b[k])) or a[k] == b[k]
             assert type(a[k]) is float
-    assert _native.score_list_alloc(0, keys) == []
+    assert _native.score_list_alloc(0, keys)[0] == []
 
 
 def test_fill_leaves_shared_objects_alone(builder):
-    """A float the caller holds is replaced, never written in place; tampered dicts still get
-    every key."""
+    """A float the caller holds is replaced, never written in place; dicts the caller changed
+    still get every key."""
     keys = ("STOI", "ESTOI")
-    lst = _native.score_list_alloc(3, keys)
+    lst, h = _native.score_list_alloc(3, keys)
     held = lst[0]["STOI"]
     lst[1]["extra"] = 1.0
     del lst[2]["STOI"]
-    _native.score_list_fill(lst, 0, np.array([[0.5, 0.25, 0.125], [1.0, 2.0, 3.0]], np.float32), keys)
+    _native.score_list_fill(h, 0, np.array([[0.5, 0.25, 0.125], [1.0, 2.0, 3.0]], np.float32), keys)
     assert math.isnan(held)
     assert lst[0] == {"STOI": 0.5, "ESTOI": 1.0}
     assert lst[1] == {"STOI": 0.25, "ESTOI": 2.0, "extra": 1.0}
     assert lst[2] == {"STOI": 0.125, "ESTOI": 3.0}
+    del h
+    import sys
+    for d in lst:  # the handle's references are gone: only the dicts' (+ getrefcount's argument)
+        refs = [sys.getrefcount(d[k]) for k in keys]  # outside the assert (its rewrite holds temporaries)
+        assert refs == [2] * len(keys)
 
 
 def test_fill_rejects_bad_input(builder):
     keys = ("PESQ",)
-    lst = _native.score_list_alloc(2, keys)
+    _, h = _native.score_list_alloc(2, keys)
     with pytest.raises(IndexError):
-        _native.score_list_fill(lst, 1, np.zeros((1, 2), np.float32), keys)
+        _native.score_list_fill(h, 1, np.zeros((1, 2), np.float32), keys)
     with pytest.raises(TypeError):
-        _native.score_list_fill(lst, 0, np.zeros((1, 2), np.int32), keys)
+        _native.score_list_fill(h, 0, np.zeros((1, 2), np.int32), keys)
+    with pytest.raises(ValueError):
+        _native.score_list_fill(h, 0, np.zeros((2, 2), np.float32), ("PESQ", "STOI"))
     with pytest.raises(ValueError):
         _native.score_list_alloc(2, ())
