@@ -43,6 +43,7 @@ sys.path.insert(0, HERE)
 
 METRIC = "utterances/sec PESQ-wb+STOI, 10s@16kHz, batch 4096, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP32_PEAK = 157.3e12  # MI355X_MICROARCH.md: FP32 vector (= f32 MFMA) peak, FLOP/s
 
 
 def parse():
@@ -204,26 +205,70 @@ def kernel_roofline(clean, noisy, reps, joint, config_batch=None):
     algo_bytes = 2 * B * L * 4  # both signals read once (2*L*4 B per pair)
     achieved = algo_bytes / (ms * 1e-3) / 1e9
     name = FRONT_KERNELS[joint]
-    traffic, source = pmc_traffic(name, B, L)
-    out = {"kernel": "pesq_front<joint>" if joint else "pesq_front", "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-           "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-           "traffic_source": source, "ms_per_launch": round(ms, 4), "algorithmic_bytes_per_launch": algo_bytes}
-    valu = pmc_counter(name, "SQ_INSTS_VALU", B, L)
-    if valu:
-        # the kernel is latency bound (2 waves per SIMD by its 256 VGPRs and 80 KB of LDS per
-        # workgroup), neither HBM nor VALU bound: its vector-ALU share = SQ_INSTS_VALU x 2
-        # cycles (a wave64 instruction on a SIMD-32, MI355X_MICROARCH.md) over the SIMDs x the
-        # measured launch time at the 2.4 GHz peak engine clock
-        n, src = valu
-        sims = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
-        out["valu_issue"] = {"instructions_per_launch": n, "frac": round(n * 2 / (sims * 2.4e9 * ms * 1e-3), 4),
-                             "source": src}
-    occ = pmc_counter(name, "waves_per_simd", B, L, as_float=True)
-    if occ:
+    summary, source = pmc_summary_for(_native.build_id(), B, L)
+    d = pmc_kernel(summary, name)
+    traffic = int(d["hbm_bytes"]) if "hbm_bytes" in d else None
+    out = {"kernel": "pesq_front<joint>" if joint else "pesq_front", "bound": None, "achieved": round(achieved, 1),
+           "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+           "traffic_source": source, "library_build_id": _native.build_id(), "ms_per_launch": round(ms, 4),
+           "algorithmic_bytes_per_launch": algo_bytes}
+    sims = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
+    cus = sims // 4
+    # what limits the kernel, from its counters (the PMC summary of THIS library build) at the
+    # measured launch time: the HBM share of its counted traffic, the vector-ALU issue share
+    # (SQ_INSTS_VALU x 2 cycles per wave64 instruction on a SIMD-32, MI355X_MICROARCH.md, over
+    # the SIMDs x the launch time at the 2.4 GHz peak clock), the LDS-array share
+    # (SQ_LDS_IDX_ACTIVE over the CUs x the launch's cycles) and the matrix pipe's
+    # (SQ_INSTS_MFMA... not collected: MFMA time is < the VALU's here)
+    limits = {}
+    if traffic:
+        limits["hbm"] = round(traffic / (ms * 1e-3) / (HBM_PEAK_GBS * 1e9), 4)
+    if "SQ_INSTS_VALU" in d:
+        limits["valu"] = round(d["SQ_INSTS_VALU"] * 2 / (sims * 2.4e9 * ms * 1e-3), 4)
+        out["valu_issue"] = {"instructions_per_launch": int(d["SQ_INSTS_VALU"]), "frac": limits["valu"],
+                             "source": source}
+    if "SQ_LDS_IDX_ACTIVE" in d:
+        limits["lds"] = round(d["SQ_LDS_IDX_ACTIVE"] / (cus * 2.4e9 * ms * 1e-3), 4)
+    if "SQ_WAIT_INST_ANY" in d and d.get("SQ_WAVE_CYCLES"):
+        # issue stalls on dependencies (mfma RAW, pipe) over the waves' lifetime (MI355X_MICROARCH.md
+        # 'rocprofv3 PMC slots'; SQ_WAIT_ANY = parked at s_waitcnt / barriers, the rest issuing)
+        limits["wait_inst_share"] = round(d["SQ_WAIT_INST_ANY"] / d["SQ_WAVE_CYCLES"], 4)
+        if "SQ_WAIT_ANY" in d:
+            limits["wait_any_share"] = round(d["SQ_WAIT_ANY"] / d["SQ_WAVE_CYCLES"], 4)
+    if "waves_per_simd" in d:
         # achieved occupancy: mean resident waves per SIMD over the launch (tools/pmc_summary.py:
         # 4 x SQ_WAVE_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)); 2 is this kernel's limit
-        out["occupancy"] = {"waves_per_simd": round(occ[0], 3), "limit": 2, "source": occ[1]}
+        out["occupancy"] = {"waves_per_simd": round(d["waves_per_simd"], 3), "limit": 2, "source": source}
+    out["limits"] = limits
+    out["bound"] = derive_bound(limits)
     return out
+
+
+def derive_bound(limits: dict) -> str:
+    """The roofline's `bound` from the counters: the resource whose share of the launch time is
+    largest among HBM traffic, VALU issue and the LDS array, if that share reaches 0.6 (a pipe
+    that busy is the limit); otherwise "latency" -- no pipe is near its peak and the kernel's
+    time goes to dependency chains, memory round trips and barriers.  "unmeasured" without a PMC
+    summary of this library build."""
+    shares = {k: limits[k] for k in ("hbm", "valu", "lds") if k in limits}
+    if not shares:
+        return "unmeasured"
+    k = max(shares, key=shares.get)
+    return k if shares[k] >= 0.6 else "latency"
+
+
+def step_roofline(B: int, L: int, ms_per_step: float) -> dict:
+    """Step-level roofline of the timed drop-in call: SURVEY 8(d)'s algorithmic bytes per step
+    (both inputs read once + 12 B of scores per pair) against HBM peak, and its informational
+    FLOPs (~23 MFLOP PESQ + ~30 MFLOP STOI per 10 s pair, scaled by length) against the FP32
+    vector peak (157.3 TFLOP/s, MI355X_MICROARCH.md)."""
+    byts = B * (2 * L * 4 + 12)
+    flops = B * 53e6 * (L / 160000)
+    s = ms_per_step * 1e-3
+    return {"algorithmic_bytes": byts, "hbm_achieved_gbs": round(byts / s / 1e9, 1),
+            "hbm_frac": round(byts / s / (HBM_PEAK_GBS * 1e9), 4), "flops": int(flops),
+            "fp32_achieved_tflops": round(flops / s / 1e12, 2), "fp32_frac": round(flops / s / FP32_PEAK, 4),
+            "ms_per_step": round(ms_per_step, 3)}
 
 
 # the uniform-length front-end instance in the PMC summaries' kernel names (joint / PESQ alone):
@@ -232,60 +277,37 @@ FRONT_KERNELS = {True: ("pesq_front<true, false, false>", "pesq_front<true, fals
                  False: ("pesq_front<false, false, false>", "pesq_front<false, false>")}
 
 
-def _pmc_meta_ok(d: dict, rows: int, L: int) -> bool:
-    """A summary recorded at `rows` x `L` per engine call ("_meta"; older summaries: 4096 x 160000)."""
-    m = d.get("_meta", {"rows_per_launch": 4096, "length": 160000})
-    return (m.get("rows_per_launch"), m.get("length")) == (rows, L)
-
-
-def pmc_counter(kernel, counter: str, B: int, L: int, as_float: bool = False):
-    """(value per launch, source) of one counter of `kernel` (a name suffix, or a tuple of them)
-    from the newest committed PMC summary recorded at B rows x L samples per launch."""
+def pmc_summary_for(build_id: str, rows: int, L: int):
+    """(summary, source) of the committed PMC summary (profiles/*/pmc_summary.json,
+    tools/pmc_summary.py) recorded on the library build `build_id` at `rows` x `L` per engine
+    call (its "_meta"), or ({}, reason).  Chosen by what was measured -- the build id of the
+    profiled library and the launch size -- never by directory names.  FETCH_SIZE x2 (gfx950
+    correction) + WRITE_SIZE per MI355X_MICROARCH.md 'HBM'; the counters need their own rocprofv3
+    passes, so they cannot be read inside the timed run."""
     import glob
-    import re
-    if L != 160000:
-        return None
-
-    def natural(path):
-        return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", path)]
-
-    best = None
-    for f in sorted(glob.glob(os.path.join(HERE, "profiles", "*", "pmc_summary.json")), key=natural):
+    found = []
+    for f in glob.glob(os.path.join(HERE, "profiles", "*", "pmc_summary*.json")):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
-        key = next((k for k in d if k.endswith(kernel)), None)
-        if key and counter in d[key] and _pmc_meta_ok(d, B, L):
-            v = d[key][counter]
-            best = (float(v) if as_float else int(v), os.path.relpath(f, HERE))
-    return best
+        m = d.get("_meta", {})
+        if (m.get("build_id"), m.get("rows_per_launch"), m.get("length")) == (build_id, rows, L):
+            found.append((os.path.relpath(f, HERE), d))
+    if not found:
+        return {}, f"none: no committed PMC summary of library build {build_id} at {rows} x {L}"
+    found.sort(key=lambda x: x[0])
+    src, d = found[0]
+    return d, src + (f" (+{len(found) - 1} more of this build)" if len(found) > 1 else "")
 
 
-def pmc_traffic(kernel, B: int, L: int):
-    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
-    (profiles/*/pmc_summary.json, tools/pmc_summary.py: FETCH_SIZE x2 gfx950 correction +
-    WRITE_SIZE, MI355X_MICROARCH.md 'HBM'), recorded at this same per-launch size (B rows x L
-    samples); the counters need their own rocprofv3 passes, so they cannot be read inside the
-    timed run."""
-    import glob
-    if L != 160000:
-        return None, None
-    best = None
-    import re
-
-    def natural(path):  # profiles/r1_v10 after profiles/r1_v9
-        return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", path)]
-
-    for f in sorted(glob.glob(os.path.join(HERE, "profiles", "*", "pmc_summary.json")), key=natural):
-        try:
-            d = json.load(open(f))
-        except (OSError, ValueError):
-            continue
-        key = next((k for k in d if k.endswith(kernel)), None)
-        if key and "hbm_bytes" in d[key] and _pmc_meta_ok(d, B, L):
-            best = (int(d[key]["hbm_bytes"]), os.path.relpath(f, HERE))
-    return best if best else (None, None)
+def pmc_kernel(summary: dict, kernel) -> dict:
+    """The counters of `kernel` (a name suffix, or a tuple of them) in a PMC summary, or {}."""
+    names = kernel if isinstance(kernel, tuple) else (kernel,)
+    for k, v in summary.items():
+        if isinstance(v, dict) and any(k.endswith(n) for n in names):
+            return v
+    return {}
 
 
 def _timed(step, args, dev, distributed):
@@ -506,6 +528,10 @@ def run_single_process(args):
 def main():
     args = parse()
     if args.single_process:
+        if args.workload != "c2":
+            print(f"bench.py: --single-process times the c2 joint drop-in call only (got --workload {args.workload})",
+                  file=sys.stderr)
+            sys.exit(2)
         run_single_process(args)
         return
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -598,7 +624,7 @@ def main():
                                        "the inputs)") + " -> list of dicts"),
                        "batch_per_gpu": B, "global_batch": world * B, "length": L, "sample_rate": 16000,
                        "parallelism": f"dp{world} (utterance shards, RCCL all-gather of scores)"},
-            "roofline": roof, "cpu_baseline": cpu, "cpu_oracle": oracle,
+            "roofline": {**roof, "step": step_roofline(B, L, ms_per_step)}, "cpu_baseline": cpu, "cpu_oracle": oracle,
             "scores_path": {"value": round(world * B * args.steps / dt_s, 2), "unit": "utterances/s",
                             "ms_per_step": round(dt_s / args.steps * 1e3, 3),
                             "what": "PESQ_STOI.scores + one device->host copy (no list of dicts)"},

@@ -256,7 +256,7 @@ class PESQ(BaseMetric):
         if self.fans_out():
             def shard(c, n, lk):
                 mos, delays = self._rows_scores(c, n, lk, sr)
-                return (mos, delays.to(torch.float32)) if aligned else mos
+                return (mos, delays.to(torch.int32)) if aligned else mos  # FanOut keeps the dtype: exact delays
 
             cols = self.fan_out(shard, clean_speech, denoised_speech, lengths, 2 if aligned else 1, balance=lengths)
             if aligned:

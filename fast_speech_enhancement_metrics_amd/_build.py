@@ -7,7 +7,9 @@ repo snapshot to the GPU box).  Cross-compiles without a GPU.
 """
 from __future__ import annotations
 
+import hashlib
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -26,8 +28,11 @@ SOURCES = ["pesq.hip", "stoi.hip", "resample.hip", "align.hip"]
 # alignment (max-ilp: 19.68 vs 19.49 ms per 4096-row aligned PESQ step)
 _ILP = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
 SOURCE_FLAGS = {"stoi.hip": _ILP, "resample.hip": _ILP}
-HEADERS = ["fsem_common.h", "fsem_fft.h", "fsem_internal.h", "fsem_resample.h", "fsem_tables.inc"]
+HEADERS = ["fsem_common.h", "fsem_fft.h", "fsem_internal.h", "fsem_resample.h", "fsem_tables.inc", "fsem_vad.h"]
+HEADER_ABI = os.path.join(PKG, "..", "include", "fsem.h")
 ARCH = os.environ.get("FSEM_OFFLOAD_ARCH", "gfx950")
+BASE_FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-Wno-unused-result"]
+_ID_MARKER = b"FSEM_BUILD_ID:"
 # the drop-in call's list-of-dicts builder (host C, CPython API; csrc/score_list.c)
 SCORE_LIST_SRC = os.path.join(CSRC, "score_list.c")
 SCORE_LIST = os.path.join(LIBDIR, "_score_list" + sysconfig.get_config_var("EXT_SUFFIX"))
@@ -40,13 +45,40 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found: the fsem HIP engine cannot be built")
 
 
+def deps() -> list:
+    """Every file whose content the library depends on."""
+    return [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [HEADER_ABI]
+
+
+def source_hash() -> str:
+    """Content hash of the sources, the headers (csrc/*.h, fsem_tables.inc, include/fsem.h) and
+    the compile flags (BASE_FLAGS, SOURCE_FLAGS): the library's build id (fsem_build_id())."""
+    h = hashlib.sha256()
+    for d in deps():
+        h.update(os.path.basename(d).encode() + b"\0")
+        with open(d, "rb") as f:
+            h.update(f.read())
+        h.update(b"\0")
+    h.update(repr((BASE_FLAGS, sorted(SOURCE_FLAGS.items()))).encode())
+    return h.hexdigest()[:16]
+
+
+def library_build_id(path: str = LIB):
+    """The build id embedded in a built library (read from the file, not loaded), or None."""
+    try:
+        with open(path, "rb") as f:
+            data = f.read()
+    except OSError:
+        return None
+    m = re.search(re.escape(_ID_MARKER) + rb"([0-9a-z]+)\0", data)
+    return m.group(1).decode() if m else None
+
+
 def _stale() -> bool:
-    if not os.path.exists(LIB):
-        return True
-    t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
-    deps.append(os.path.join(PKG, "..", "include", "fsem.h"))
-    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+    """True when libfsem.so is missing or was built from other sources or flags than the tree's
+    (content hash: an edited header or a changed SOURCE_FLAGS entry rebuilds; a touched file
+    whose content is unchanged does not)."""
+    return library_build_id(LIB) != source_hash()
 
 
 def build(force: bool = False, verbose: bool = False, stamps: bool = False) -> str:
@@ -54,25 +86,34 @@ def build(force: bool = False, verbose: bool = False, stamps: bool = False) -> s
     if not force and not stamps and not _stale():
         return LIB
     os.makedirs(LIBDIR, exist_ok=True)
-    objdir = os.path.join(LIBDIR, "obj" + ("_stamps" if stamps else ""))
+    # per-process object directory and temporary library: concurrent builds do not overwrite
+    # each other's objects; the finished library replaces the old one atomically
+    objdir = os.path.join(LIBDIR, f"obj{'_stamps' if stamps else ''}.{os.getpid()}")
     os.makedirs(objdir, exist_ok=True)
-    base = [_hipcc(), "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-Wno-unused-result"]
+    base = [_hipcc()] + BASE_FLAGS + [f'-DFSEM_BUILD_ID="{source_hash()}"']
     if stamps:
         base.append("-DFSEM_STAMPS")
     objs = []
-    for src in SOURCES:  # one object per source (per-source flags), then one shared library
-        obj = os.path.join(objdir, src.replace(".hip", ".o"))
-        cmd = base + SOURCE_FLAGS.get(src, []) + ["-c", "-o", obj, os.path.join(CSRC, src)]
+    try:
+        procs = []
+        for src in SOURCES:  # one object per source (per-source flags, compiled in parallel), one library
+            obj = os.path.join(objdir, src.replace(".hip", ".o"))
+            cmd = base + SOURCE_FLAGS.get(src, []) + ["-c", "-o", obj, os.path.join(CSRC, src)]
+            if verbose:
+                print(" ".join(cmd))
+            procs.append((subprocess.Popen(cmd, cwd=CSRC), cmd))
+            objs.append(obj)
+        for p, cmd in procs:
+            if p.wait() != 0:
+                raise subprocess.CalledProcessError(p.returncode, cmd)
+        tmp = f"{lib}.{os.getpid()}.tmp"
+        cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs
         if verbose:
             print(" ".join(cmd))
         subprocess.check_call(cmd, cwd=CSRC)
-        objs.append(obj)
-    tmp = lib + ".tmp"
-    cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs
-    if verbose:
-        print(" ".join(cmd))
-    subprocess.check_call(cmd, cwd=CSRC)
-    os.replace(tmp, lib)
+        os.replace(tmp, lib)
+    finally:
+        shutil.rmtree(objdir, ignore_errors=True)
     return lib
 
 

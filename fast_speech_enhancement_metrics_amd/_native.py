@@ -14,7 +14,8 @@ import threading
 import torch
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("FSEM_LIB", os.path.join(_PKG, "lib", "libfsem.so"))
+_DEFAULT_LIB = os.path.join(_PKG, "lib", "libfsem.so")
+LIB_PATH = os.environ.get("FSEM_LIB", _DEFAULT_LIB)
 
 FSEM_OK = 0
 FSEM_EINVAL = -1
@@ -35,6 +36,7 @@ _vp = ctypes.c_void_p
 SIGNATURES = {
     "fsem_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "fsem_version": (ctypes.c_int, []),
+    "fsem_build_id": (ctypes.c_char_p, []),
     "fsem_resample_length": (_c_i64, [_c_i64, _c_i32, _c_i32]),
     "fsem_resample_f32": (ctypes.c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _c_i64, _c_i32, _c_i32, _vp]),
     "fsem_resample_rows_f32": (ctypes.c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_i64, _c_i32, _c_i32, _vp]),
@@ -173,8 +175,37 @@ class NativeError(RuntimeError):
     pass
 
 
+def _check_build_id() -> None:
+    """The in-tree library must be the build of this tree's sources and flags (_build.source_hash,
+    embedded as fsem_build_id()): a stale library is rebuilt where hipcc is available, else the
+    load fails loudly -- no kernel runs from a binary the committed sources did not produce.
+    FSEM_LIB (a library variant chosen explicitly, tools/ab_*.py) is not checked."""
+    if LIB_PATH != _DEFAULT_LIB:
+        return
+    from . import _build
+    if not all(os.path.exists(d) for d in _build.deps()):
+        return  # no source tree next to the package (nothing to compare with)
+    want = _build.source_hash()
+    have = _build.library_build_id(LIB_PATH)
+    if have == want:
+        return
+    try:
+        _build.build(force=True)
+    except Exception as exc:  # noqa: BLE001 -- any build failure: refuse the stale binary
+        raise ImportError(f"fsem HIP engine {LIB_PATH} is stale (build id {have}, sources {want}) and could not "
+                          f"be rebuilt: {exc!r}") from exc
+    have = _build.library_build_id(LIB_PATH)
+    if have != want:
+        raise ImportError(f"fsem HIP engine {LIB_PATH}: build id {have} after rebuilding, sources {want}")
+
+
+def build_id() -> str:
+    """The loaded library's build id (fsem_build_id())."""
+    return load().fsem_build_id().decode()
+
+
 def load() -> ctypes.CDLL:
-    """Load (once) and return the library; raises if it is missing."""
+    """Load (once) and return the library; raises if it is missing or stale."""
     global _lib
     if _lib is not None:
         return _lib
@@ -184,6 +215,7 @@ def load() -> ctypes.CDLL:
                 raise ImportError(
                     f"fsem HIP engine not built: {LIB_PATH} is missing "
                     "(run `python -m fast_speech_enhancement_metrics_amd._build`)")
+            _check_build_id()
             lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_LOCAL)
             for name, (res, args) in SIGNATURES.items():
                 fn = getattr(lib, name)

@@ -64,9 +64,16 @@ class BaseMetric(ABC):
         audio = torch.atleast_2d(audio)
         if self.fans_out() and self.sample_rate == self.EXPECTED_SAMPLING_RATE:
             return audio
-        audio = audio.to(self.home_device())
+        home = self.home_device()
+        audio = audio.to(home)
         if self.sample_rate != self.EXPECTED_SAMPLING_RATE:
-            audio = self.resampler(audio, lengths)
+            if self.devices is not None:
+                # the engine launches on the current HIP device (include/fsem.h): make the home
+                # device current while its stream resamples (devices=[1, ...] called with 0 current)
+                with torch.cuda.device(home):
+                    audio = self.resampler(audio, lengths)
+            else:
+                audio = self.resampler(audio, lengths)
         return audio
 
     def prepare_inputs(self, clean_speech: torch.Tensor | None, denoised_speech: torch.Tensor,

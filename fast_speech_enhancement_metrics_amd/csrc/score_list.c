@@ -99,6 +99,7 @@ done:
  * reference each, so none can be freed behind the handle's back). */
 typedef struct {
   PyObject *lst;
+  PyObject *keys; /* the allocation's keys: score_list_fill must pass equal ones */
   Py_ssize_t B, K;
   PyObject **f; /* B x K */
 } Pending;
@@ -111,6 +112,7 @@ static void pending_free(PyObject *cap) {
     PyMem_Free(p->f);
   }
   Py_XDECREF(p->lst);
+  Py_XDECREF(p->keys);
   PyMem_Free(p);
 }
 
@@ -143,6 +145,8 @@ static PyObject *score_list_alloc(PyObject *self, PyObject *args) {
   }
   p->B = B;
   p->K = K;
+  Py_INCREF(keys);
+  p->keys = keys;
   for (Py_ssize_t b = 0; b < B; ++b) {
     PyObject *d = PyDict_New();
     if (!d) goto fail;
@@ -170,7 +174,15 @@ static PyObject *score_list_fill(PyObject *self, PyObject *args) {
   if (!p) return NULL;
   const Py_ssize_t K = check_keys(keys);
   if (K < 0) return NULL;
-  if (K != p->K) {
+  /* the same keys, element by element (as the Python form's tuple comparison): the in-place
+   * path writes through the allocation's float objects, which belong to the allocation's keys */
+  int same = K == p->K;
+  for (Py_ssize_t k = 0; same && k < K; ++k) {
+    const int eq = PyObject_RichCompareBool(PyTuple_GET_ITEM(keys, k), PyTuple_GET_ITEM(p->keys, k), Py_EQ);
+    if (eq < 0) return NULL;
+    same = eq;
+  }
+  if (!same) {
     PyErr_SetString(PyExc_ValueError, "score_list_fill: keys differ from the allocation's");
     return NULL;
   }

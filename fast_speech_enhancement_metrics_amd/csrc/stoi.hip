@@ -950,4 +950,12 @@ extern "C" const char *fsem_strerror(int code) {
   }
 }
 
-extern "C" int fsem_version(void) { return 5; }  // 5: + fsem_time_align_utt_*; 4: + fsem_pre_emphasize_f32; 3: + fsem_time_align_*, fsem_pesq_distances_*
+extern "C" int fsem_version(void) { return 6; }  // 6: + fsem_build_id; 5: + fsem_time_align_utt_*; 4: + fsem_pre_emphasize_f32; 3: + fsem_time_align_*, fsem_pesq_distances_*
+
+// The build's content hash (_build.py passes -DFSEM_BUILD_ID); the marker prefix lets the host
+// layer read the id from the file without loading it (_build.library_build_id).
+#ifndef FSEM_BUILD_ID
+#define FSEM_BUILD_ID "unknown"
+#endif
+static const char kBuildIdMarker[] = "FSEM_BUILD_ID:" FSEM_BUILD_ID;
+extern "C" const char *fsem_build_id(void) { return kBuildIdMarker + 14; }

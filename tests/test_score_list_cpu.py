@@ -169,3 +169,18 @@ def test_fill_rejects_bad_input(builder):
         _native.score_list_fill(h, 0, np.zeros((2, 2), np.float32), ("PESQ", "STOI"))
     with pytest.raises(ValueError):
         _native.score_list_alloc(2, ())
+
+
+def test_fill_rejects_mismatched_keys_of_equal_count(builder):
+    """Both builders refuse keys that differ from the allocation's in any element (the native
+    in-place path writes through the allocation's float objects, so a different key tuple of the
+    same length must not be accepted); equal keys in a new tuple object are fine."""
+    keys = ("STOI", "ESTOI")
+    lst, h = _native.score_list_alloc(2, keys)
+    scores = np.array([[0.5, 0.25], [1.0, 2.0]], np.float32)
+    for bad in (("ESTOI", "STOI"), ("STOI", "PESQ"), ("PESQ", "ESTOI")):
+        with pytest.raises(ValueError, match="keys differ"):
+            _native.score_list_fill(h, 0, scores, bad)
+    assert all(math.isnan(v) for d in lst for v in d.values())  # nothing written by the refused calls
+    _native.score_list_fill(h, 0, scores, tuple(["STOI", "E" + "STOI"]))
+    assert lst == [{"STOI": 0.5, "ESTOI": 1.0}, {"STOI": 0.25, "ESTOI": 2.0}]

@@ -6,8 +6,9 @@ Per fsem kernel, averaged over its launches: raw counter values, plus HBM bytes 
 MI355X_MICROARCH.md 'HBM' prescribes: FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950
 FETCH_SIZE counts half the bytes of wide (16 B/lane) coalesced streaming reads, so
 hbm_read_bytes = 2 * 1024 * FETCH_SIZE; hbm_write_bytes = 1024 * WRITE_SIZE.  "_meta" records the
-rows and length of one profiled engine call (env PMC_ROWS / PMC_LENGTH, set by the drivers);
-bench.py only takes counters recorded at its own per-launch size.
+rows and length of one profiled engine call (env PMC_ROWS / PMC_LENGTH, set by the drivers) and
+the build id of the profiled library; bench.py only takes counters recorded on its own library
+build at its own per-launch size.
 """
 import collections
 import csv
@@ -46,8 +47,14 @@ def main(root: str):
             d["waves_per_simd"] = 4 * d["SQ_WAVE_CYCLES"] / (d["GRBM_GUI_ACTIVE"] / 8 * 1024)
         out[k] = d
     # the engine call the passes profiled (tools/one_step.py: the drop-in call's row chunk)
+    # and the library build it ran (fsem_build_id, read from the file the passes loaded: FSEM_LIB
+    # or the in-tree libfsem.so): bench.py takes counters of its own build and size only
+    sys.path.insert(0, os.path.abspath(os.path.join(os.path.dirname(__file__), "..")))
+    from fast_speech_enhancement_metrics_amd import _build
+    lib = os.environ.get("FSEM_LIB", _build.LIB)
     out["_meta"] = {"rows_per_launch": int(os.environ.get("PMC_ROWS", "4096")),
-                    "length": int(os.environ.get("PMC_LENGTH", "160000"))}
+                    "length": int(os.environ.get("PMC_LENGTH", "160000")),
+                    "build_id": _build.library_build_id(lib), "library": os.path.basename(lib)}
     json.dump(out, sys.stdout, indent=1, sort_keys=True)
     print()
 
