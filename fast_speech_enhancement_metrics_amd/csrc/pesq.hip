@@ -38,6 +38,7 @@
 #include <algorithm>
 #include <atomic>
 #include <mutex>
+#include <type_traits>
 
 #include "fsem_fft.h"
 #include "fsem_internal.h"
@@ -69,7 +70,15 @@ constexpr int NF = 48;            // frames per segment
 constexpr int OWN = NF * 256;     // samples of band-pass power owned per segment
 constexpr int NBARK = 49;
 constexpr int NS = 12;            // scan states: 10 band-pass (5 sections) + 2 pre-emphasis
-constexpr int SCAN_LD = 13;       // floats per lane in the scan buffer (odd: conflict-free)
+// floats per lane in the scan buffer: 12 (the states as three 16-byte words: ds_read_b128 /
+// ds_write_b128, conflict-free at a 48-byte stride -- lanes l, l + 16 share banks, and the
+// b128 lane groups hold distinct l mod 16; one LDS round trip per scan level instead of six
+// ds_read2_b32 waited for one by one); 13 (odd, b32 accesses) with FSEM_SCAN_B32
+#ifdef FSEM_SCAN_B32
+constexpr int SCAN_LD = 13;
+#else
+constexpr int SCAN_LD = 12;
+#endif
 // exchange buffer: 4 waves x 512 complex for the FFTs, the resampler's per-wave staging slices
 // (4 x 960 floats, joint entry), or the two buffers of the double-buffered chunk scan.  Scan
 // buffer A keeps wave w's states inside wave w's own staging slice (960 w + 13 lane: no wave
@@ -77,14 +86,15 @@ constexpr int SCAN_LD = 13;       // floats per lane in the scan buffer (odd: co
 // resampler and the scan); buffer B (first written after a barrier) is packed after A's last
 // state.  With the tile, 81 568 B per workgroup: 2 fit a CU.
 constexpr int SCAN_A_WAVE = 960;                               // = the resampler's RS_STAGE
-constexpr int SCAN_B0 = 3 * SCAN_A_WAVE + 64 * 13;             // 3712: just past buffer A
-constexpr int XBUF = SCAN_B0 + PT * 13;                        // 7040 floats
+constexpr int SCAN_B0 = 3 * SCAN_A_WAVE + 64 * SCAN_LD;        // just past buffer A
+constexpr int XBUF = 3 * SCAN_A_WAVE + 64 * 13 + PT * 13;      // 7040 floats
 static_assert(XBUF >= 4 * 2 * kFftBuf, "FFT exchange areas fit");
 constexpr int SPEC_LD = 258;      // parked spectrum row stride: = 2 mod 32, MFMA A reads conflict-free
 constexpr int NBP = 10;           // band-pass states
 constexpr int PF = TILE / 4 / PT; // float4 per thread per tile
 static_assert(WARM + 256 * (NF + 1) == TILE, "tile geometry");
-static_assert(SCAN_LD == 13 && 64 * SCAN_LD <= SCAN_A_WAVE, "scan buffer A: a wave's states within its staging slice");
+static_assert(64 * SCAN_LD <= SCAN_A_WAVE && SCAN_B0 + PT * SCAN_LD <= XBUF && (SCAN_B0 * 4) % 16 == 0,
+              "scan buffer A: a wave's states within its staging slice; B within the exchange buffer");
 static_assert(SPEC_LD * (NF - 1) + 256 <= TILE, "parked spectra stay in the tile");
 static_assert(TILE % (4 * PT) == 0, "tile load split");
 
@@ -167,6 +177,22 @@ __device__ __forceinline__ float wave_max_pos(float v) {
   e = max(e, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)e, 0x142, 0xA, 0xF, false));  // row_bcast:15
   e = max(e, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)e, 0x143, 0xC, 0xF, false));  // row_bcast:31
   return __uint_as_float(__builtin_amdgcn_readlane(e, 63));
+}
+
+// Wave sum by DPP (row rotations 1, 2, 4, 8 -- every lane then holds its row's sum -- and two
+// row broadcasts), read from lane 63: no LDS round trip (the butterfly of __shfl_xor is six
+// ds_bpermute waited for one by one).  A fixed summation order, deterministic.
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  auto rot = [](float x, auto ctrl) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), decltype(ctrl)::value, 0xF, 0xF, false));
+  };
+  v += rot(v, std::integral_constant<int, 0x121>{});  // row_ror:1
+  v += rot(v, std::integral_constant<int, 0x122>{});  // row_ror:2
+  v += rot(v, std::integral_constant<int, 0x124>{});  // row_ror:4
+  v += rot(v, std::integral_constant<int, 0x128>{});  // row_ror:8
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x142, 0xA, 0xF, false));  // row_bcast:15
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x143, 0xC, 0xF, false));  // row_bcast:31
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 
 struct Item {
@@ -259,7 +285,9 @@ template <bool TAPER>
 __device__ __forceinline__ void iir_pass1(const float4 *__restrict__ my4, int64_t t_lane, int64_t L, float h1,
                                           float d1, float hr, float e[NS]) {
   const float tf0 = (float)t_lane, Lf = (float)L;
-  // opaque table pointer: the rows stay memory operands (s_load) instead of folded literals
+  // opaque table pointer: the rows stay memory operands (s_load) instead of folded literals.
+  // (Measured in round 5: the rows from an LDS copy by broadcast ds_read_b128 instead -- no
+  // SGPR streaming -- made the joint front end 13 % slower rolled, 27 % unrolled)
   uint64_t gaddr = reinterpret_cast<uint64_t>(&kScanG[0][0]);
   asm volatile("" : "+s"(gaddr));
   typedef const __attribute__((address_space(4))) float crow[NS];
@@ -787,8 +815,31 @@ __global__ void __launch_bounds__(PT, 2)
     auto scan_at = [&](bool in_b, int t) {
       return in_b ? xbuf + SCAN_B0 + t * SCAN_LD : xbuf + SCAN_A_WAVE * (t >> 6) + (t & 63) * SCAN_LD;
     };
+    // the 12 states of a lane as float4 words (SCAN_LD = 12) or single floats (13)
+    auto put_states = [&](float *dst) {
+      if (SCAN_LD == 12) {
+        float4 *d4 = reinterpret_cast<float4 *>(dst);
+        d4[0] = make_float4(e[0], e[1], e[2], e[3]);
+        d4[1] = make_float4(e[4], e[5], e[6], e[7]);
+        d4[2] = make_float4(e[8], e[9], e[10], e[11]);
+      } else {
 #pragma unroll
-    for (int i = 0; i < NS; ++i) scan_at(false, tid)[i] = e[i];
+        for (int i = 0; i < NS; ++i) dst[i] = e[i];
+      }
+    };
+    auto get_states = [&](const float *src, float keep, float q[NS]) {
+      if (SCAN_LD == 12) {
+        const float4 *s4 = reinterpret_cast<const float4 *>(src);
+        const float4 a = s4[0], b = s4[1], c = s4[2];
+        const float v[NS] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w};
+#pragma unroll
+        for (int i = 0; i < NS; ++i) q[i] = v[i] * keep;
+      } else {
+#pragma unroll
+        for (int i = 0; i < NS; ++i) q[i] = src[i] * keep;
+      }
+    };
+    put_states(scan_at(false, tid));
     lds_barrier();
 #pragma unroll
     for (int lv = 0; lv < 4; ++lv) {
@@ -796,8 +847,7 @@ __global__ void __launch_bounds__(PT, 2)
       float q[NS];
       const float *src = scan_at(lv & 1, max(tid - d, 0));  // one base + immediate offsets
       const float keep = (tid >= d) ? 1.f : 0.f;
-#pragma unroll
-      for (int i = 0; i < NS; ++i) q[i] = src[i] * keep;
+      get_states(src, keep, q);
 #pragma unroll
       for (int i = 0; i < NBP; ++i) {
         float acc = e[i];
@@ -812,9 +862,7 @@ __global__ void __launch_bounds__(PT, 2)
         e[NBP] = p0;
         e[NBP + 1] = p1;
       }
-      float *dst = scan_at(!(lv & 1), tid);
-#pragma unroll
-      for (int i = 0; i < NS; ++i) dst[i] = e[i];
+      put_states(scan_at(!(lv & 1), tid));
       lds_barrier();
     }
     // start state of chunk j = inclusive prefix of chunk j-1 (level 3 wrote buffer A)
@@ -822,8 +870,7 @@ __global__ void __launch_bounds__(PT, 2)
     {
       const float *src = scan_at(false, max(tid - 1, 0));
       const float keep = (tid >= 1) ? 1.f : 0.f;
-#pragma unroll
-      for (int i = 0; i < NS; ++i) z[i] = src[i] * keep;
+      get_states(src, keep, z);
       // pre-emphasis: scan basis (u, v) -> direct-form states (y[n-1], y[n-2]) (gen_tables.py)
       const float u = z[NBP], v = z[NBP + 1];
       z[NBP] = fmaf(kPreToY[0][0], u, kPreToY[0][1] * v);
@@ -871,7 +918,11 @@ __global__ void __launch_bounds__(PT, 2)
       else
         acc = iir_pass2_masked<false>(w4, z, own_lo, own_hi, lim, t_lane, L, xm1, xm1 - xm2);
       // per-wave partials (no workgroup barrier); pesq_power_sum adds them in a fixed order
+#ifdef FSEM_WAVE_SUM_SHFL
       const float tot = wave_sum(acc);
+#else
+      const float tot = wave_sum_dpp(acc);
+#endif
       if (lane == 0) ppart[(it.s * nseg + g) * 4 + wave] = tot * (kBpGain * kBpGain);
     }
     lds_barrier();
