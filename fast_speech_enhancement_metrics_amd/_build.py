@@ -27,7 +27,13 @@ SOURCES = ["pesq.hip", "stoi.hip", "resample.hip", "align.hip"]
 # default, under which it does not spill (max-ilp: 476 SGPR spills), and so does the time
 # alignment (max-ilp: 19.68 vs 19.49 ms per 4096-row aligned PESQ step)
 _ILP = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
-SOURCE_FLAGS = {"stoi.hip": _ILP, "resample.hip": _ILP}
+# pesq.hip without the SLP vectoriser (round 5): it paired scalar FMAs with literal constants
+# into v_pk_fma_f32 whose constant pairs each cost two s_mov_b32 (the chunk scan: 243 of its 468
+# instructions); the kernels are issue bound (every issued instruction, SALU included, costs the
+# wave ~4 cycles: SQ_ACTIVE_INST_SCA / SQ_INSTS_SALU = 1 quad-cycle), and the packed forms that
+# pay (FFT butterflies, pass 1's functionals, pass 2's cascade) are written out explicitly.
+# Joint front end 4.478 -> 4.392 ms per 4096-row launch, profiles/r5_pk/
+SOURCE_FLAGS = {"pesq.hip": ["-fno-slp-vectorize"], "stoi.hip": _ILP, "resample.hip": _ILP}
 HEADERS = ["fsem_common.h", "fsem_fft.h", "fsem_internal.h", "fsem_resample.h", "fsem_tables.inc", "fsem_vad.h"]
 HEADER_ABI = os.path.join(PKG, "..", "include", "fsem.h")
 ARCH = os.environ.get("FSEM_OFFLOAD_ARCH", "gfx950")

@@ -290,12 +290,17 @@ __device__ __forceinline__ void iir_pass1(const float4 *__restrict__ my4, int64_
   // SGPR streaming -- made the joint front end 13 % slower rolled, 27 % unrolled)
   uint64_t gaddr = reinterpret_cast<uint64_t>(&kScanG[0][0]);
   asm volatile("" : "+s"(gaddr));
-  typedef const __attribute__((address_space(4))) float crow[NS];
-  crow *G = reinterpret_cast<crow *>(gaddr);
+  // the 12 functionals as six packed pairs (states 2j, 2j + 1): one v_pk_fma_f32 per pair and
+  // sample with the pair's SGPR operand straight from the scalar loads, written out rather than
+  // left to the SLP vectoriser (which pesq.hip is compiled without: it paired literal constants
+  // into SGPRs with two s_mov_b32 each elsewhere, _build.SOURCE_FLAGS)
+  typedef float pf2v __attribute__((ext_vector_type(2)));
+  typedef const __attribute__((address_space(4))) pf2v crow2[NS / 2];
+  crow2 *G = reinterpret_cast<crow2 *>(gaddr);
+  pf2v ep[NS / 2];
 #pragma unroll
-  for (int i = 0; i < NBP; ++i) e[i] = kScanB[i] * hr;  // S x[-1] (untapered)
-  e[NBP] = kScanB[NBP] * d1;                            // -G2[0] d[-1] (tapered)
-  e[NBP + 1] = kScanB[NBP + 1] * d1;
+  for (int j = 0; j < NBP / 2; ++j) ep[j] = (pf2v){kScanB[2 * j], kScanB[2 * j + 1]} * hr;  // S x[-1] (untapered)
+  ep[NBP / 2] = (pf2v){kScanB[NBP], kScanB[NBP + 1]} * d1;                                // -G2[0] d[-1] (tapered)
   float xr = hr;  // previous raw sample (TAPER: the band-pass's own history)
 #pragma unroll
   for (int q = 0; q < CH / 4; ++q) {
@@ -317,10 +322,14 @@ __device__ __forceinline__ void iir_pass1(const float4 *__restrict__ my4, int64_
         h1 = xs[c];
       }
 #pragma unroll
-      for (int i = 0; i < NBP; ++i) e[i] = fmaf(G[n][i], db, e[i]);
-      e[NBP] = fmaf(G[n][NBP], dp, e[NBP]);
-      e[NBP + 1] = fmaf(G[n][NBP + 1], dp, e[NBP + 1]);
+      for (int j = 0; j < NBP / 2; ++j) ep[j] = __builtin_elementwise_fma(G[n][j], (pf2v){db, db}, ep[j]);
+      ep[NBP / 2] = __builtin_elementwise_fma(G[n][NBP / 2], (pf2v){dp, dp}, ep[NBP / 2]);
     }
+  }
+#pragma unroll
+  for (int j = 0; j < NS / 2; ++j) {
+    e[2 * j] = ep[j].x;
+    e[2 * j + 1] = ep[j].y;
   }
 }
 
