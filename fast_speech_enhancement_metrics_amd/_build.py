@@ -20,21 +20,23 @@ CSRC = os.path.join(PKG, "csrc")
 LIBDIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIBDIR, "libfsem.so")
 STAMP_LIB = os.path.join(LIBDIR, "libfsem_stamps.so")  # diagnostic build (tools/stamps.py)
-SOURCES = ["pesq.hip", "stoi.hip", "resample.hip", "align.hip"]
+SOURCES = ["pesq.hip", "pesq_back.hip", "stoi.hip", "resample.hip", "align.hip"]
 # per-source code-generation flags: the STOI kernels and the resamplers are scheduled for ILP
 # (gfx950's max-ilp machine scheduler: joint call 7.167 vs 7.198 ms, profiles/r4_sc/; config 5
 # 224.0k vs 221.3k utt/s, profiles/r4_fl/; bitwise equal); the PESQ front end keeps the
 # default, under which it does not spill (max-ilp: 476 SGPR spills), and so does the time
 # alignment (max-ilp: 19.68 vs 19.49 ms per 4096-row aligned PESQ step)
 _ILP = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
-# pesq.hip without the SLP vectoriser (round 5): it paired scalar FMAs with literal constants
+# pesq.hip (the front end) without the SLP vectoriser (round 5): it paired scalar FMAs with literal constants
 # into v_pk_fma_f32 whose constant pairs each cost two s_mov_b32 (the chunk scan: 243 of its 468
 # instructions); the kernels are issue bound (every issued instruction, SALU included, costs the
 # wave ~4 cycles: SQ_ACTIVE_INST_SCA / SQ_INSTS_SALU = 1 quad-cycle), and the packed forms that
 # pay (FFT butterflies, pass 1's functionals, pass 2's cascade) are written out explicitly.
-# Joint front end 4.478 -> 4.392 ms per 4096-row launch, profiles/r5_pk/
+# Joint front end 4.478 -> 4.392 ms per 4096-row launch, profiles/r5_pk/.  The back end
+# (pesq_back.hip) keeps it: its 49-band loops pack into fewer instructions with it.
 SOURCE_FLAGS = {"pesq.hip": ["-fno-slp-vectorize"], "stoi.hip": _ILP, "resample.hip": _ILP}
-HEADERS = ["fsem_common.h", "fsem_fft.h", "fsem_internal.h", "fsem_resample.h", "fsem_tables.inc", "fsem_vad.h"]
+HEADERS = ["fsem_common.h", "fsem_fft.h", "fsem_internal.h", "fsem_pesq.h", "fsem_resample.h", "fsem_tables.inc",
+           "fsem_vad.h"]
 HEADER_ABI = os.path.join(PKG, "..", "include", "fsem.h")
 ARCH = os.environ.get("FSEM_OFFLOAD_ARCH", "gfx950")
 BASE_FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-Wno-unused-result"]

@@ -17,7 +17,7 @@ if [ -n "$REV" ]; then
 fi
 C=$SRC/fast_speech_enhancement_metrics_amd/csrc
 T=$(mktemp -d)
-for f in pesq stoi resample align; do
+for f in pesq pesq_back stoi resample align; do
   [ -f "$C/$f.hip" ] || continue
   FL=""
   { [ "$f" = "stoi" ] || [ "$f" = "resample" ]; } && FL="-mllvm -amdgpu-sched-strategy=max-ilp"
