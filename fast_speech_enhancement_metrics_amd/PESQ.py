@@ -311,6 +311,4 @@ class PESQ(BaseMetric):
             mos = self.scores(clean_speech, denoised_speech, lengths, sample_rate=self.EXPECTED_SAMPLING_RATE)
             if not mos.is_cuda:
                 return _native.score_list(mos.reshape(1, -1), ("PESQ",))
-            res, h = _native.score_list_alloc(mos.numel(), ("PESQ",))  # while the GPU computes
-            _native.score_list_fill(h, 0, mos.reshape(1, -1).cpu(), ("PESQ",))
-            return res
+            return _native.list_from_device(self, mos.reshape(1, -1), ("PESQ",))[0]

@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import warnings
 
+import numpy as np
 import torch
 
 from . import _cpu, _native
@@ -205,16 +206,15 @@ class STOI(BaseMetric):
 
     def _finish(self, stois: torch.Tensor, estois: torch.Tensor) -> list[dict[str, float]]:
         t = torch.stack([stois.float(), estois.float()])
-        # on the GPU the dicts are built while it computes, then filled
-        res, h = _native.score_list_alloc(t.shape[1], ("STOI", "ESTOI")) if t.is_cuda else (None, None)
-        t = t.cpu()
-        if bool(torch.isnan(t[0]).all()):  # no utterance has a 30-frame segment (STOI.py:162-165)
+        if t.is_cuda:  # the dicts are built while the GPU computes, then filled
+            res, host = _native.list_from_device(self, t, ("STOI", "ESTOI"))
+            nan_all = bool(np.isnan(host[0]).all())
+        else:
+            res, nan_all = None, bool(torch.isnan(t[0]).all())
+        if nan_all:  # no utterance has a 30-frame segment (STOI.py:162-165)
             warnings.warn("Not enough non-silent frames. Please check your sound files", RuntimeWarning, stacklevel=3)
             raise TypeError("iteration over a 0-d tensor")
-        if res is None:
-            return _native.score_list(t, ("STOI", "ESTOI"))
-        _native.score_list_fill(h, 0, t, ("STOI", "ESTOI"))
-        return res
+        return res if res is not None else _native.score_list(t, ("STOI", "ESTOI"))
 
     def _resample_cpu(self, x: torch.Tensor, sr: int) -> torch.Tensor:
         if sr == self.sample_rate:
