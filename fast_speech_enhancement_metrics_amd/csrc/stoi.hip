@@ -417,7 +417,7 @@ __global__ void __launch_bounds__(64 * TOB_WAVES)
   const int plane = (64 - lane) & 63;
   const int pc_sig = kObmPiece[lane][0], pc_band = kObmPiece[lane][1];
   const int pc_lo = kObmPiece[lane][2], pc_hi = kObmPiece[lane][3];
-  const int pc_end = kObmPiece[lane][4];
+  const int pc_gs = kObmPiece[lane][4];
   const bool pc_head = kObmPiece[lane][5] != 0;
   // Two consecutive STFT frames of ONE signal per complex FFT (z = frame a + i frame b): the
   // Hermitian split recovers each from Z[k] -/+ conj(Z[N-k]), whose rounding is relative to |Z|
@@ -511,14 +511,17 @@ __global__ void __launch_bounds__(64 * TOB_WAVES)
       const float *ps = pbuf + 256 * pc_sig;
       float acc = (pc_lo < pc_hi) ? ps[pc_lo] : 0.f;
 #pragma unroll
-      for (int i = 1; i < 9; ++i) {  // unconditional reads (inside the frame's 256 powers), masked adds
+      for (int i = 1; i < 12; ++i) {  // unconditional reads (inside the frame's 256 powers), masked adds
         const float x = ps[pc_lo + i];
         acc += (pc_lo + i < pc_hi) ? x : 0.f;
       }
-#pragma unroll
-      for (int off = 1; off < 8; off <<= 1) {
-        const float v = __shfl_down(acc, off, 64);
-        if (lane + off < pc_end) acc += v;
+      // each band's group (1, 2 or 4 lanes, aligned inside a 16-lane row): two in-row DPP steps
+      // (row_shl k: lane l reads lane l + k), no LDS round trip
+      {
+        const float a1 = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, acc), 0x101, 0xF, 0xF, true));
+        acc += (pc_gs >= 2) ? a1 : 0.f;
+        const float a2 = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, acc), 0x102, 0xF, 0xF, true));
+        acc += (pc_gs >= 4) ? a2 : 0.f;
       }
       // hardware square root (1 ulp; the correctly rounded sqrtf is a ~17-instruction sequence
       // that every lane of the wave issues)
@@ -539,15 +542,22 @@ __global__ void __launch_bounds__(64 * TOB_WAVES)
 // v_pk_add_f32 / v_pk_mul_f32: twice the v_fma_f32 rate on gfx950).  The per-lane row
 // statistics of the ESTOI time normalisation stay in registers (uniform-index writes from the
 // rolled band loop).
-constexpr int SEG_T = 128;
+#ifndef FSEM_SEG_T
+#define FSEM_SEG_T 128
+#endif
+#ifndef FSEM_SEG_OCC
+#define FSEM_SEG_OCC 3
+#endif
+constexpr int SEG_T = FSEM_SEG_T;
+constexpr int SEG_WAVES = SEG_T / 64;
 typedef float f2 __attribute__((ext_vector_type(2)));
-__global__ void __launch_bounds__(SEG_T, 3)
+__global__ void __launch_bounds__(SEG_T, FSEM_SEG_OCC)
     stoi_seg(const float *__restrict__ tob, int64_t B, int64_t tmax, const int *__restrict__ kept,
              double *__restrict__ part, int P, int64_t b0) {
   constexpr int W = SEG_T + NSEG;  // frames per pass
   constexpr int LDX = W + 1;
   __shared__ f2 XY[NB][LDX];
-  __shared__ double red[4];
+  __shared__ double red[2 * SEG_WAVES];
   const int tid = threadIdx.x;
   const int64_t b = b0 + blockIdx.y;
   const int p = blockIdx.x;
@@ -679,7 +689,7 @@ __global__ void __launch_bounds__(SEG_T, 3)
       et += (double)e_acc;
     }
   }
-  // deterministic 2-wave reduction
+  // deterministic reduction over the workgroup's waves, in wave order
   st = wave_sum_d(st);
   et = wave_sum_d(et);
   lds_barrier();
@@ -689,8 +699,14 @@ __global__ void __launch_bounds__(SEG_T, 3)
   }
   lds_barrier();
   if (tid == 0) {
-    part[(b * P + p) * 2] = red[0] + red[2];
-    part[(b * P + p) * 2 + 1] = red[1] + red[3];
+    double a = red[0], e = red[1];
+#pragma unroll
+    for (int w = 1; w < SEG_WAVES; ++w) {
+      a += red[2 * w];
+      e += red[2 * w + 1];
+    }
+    part[(b * P + p) * 2] = a;
+    part[(b * P + p) * 2 + 1] = e;
   }
 }
 
