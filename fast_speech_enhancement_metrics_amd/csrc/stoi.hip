@@ -535,15 +535,18 @@ __global__ void __launch_bounds__(64 * TOB_WAVES)
 }
 
 // One lane per 30-frame segment m: x[j][t] = X[j][m + t], y likewise (STOI.py:121-198).
-// 128-lane workgroups, one per (utterance, block of 128 segments): grid (B, P), so a short
+// SEG_T-lane workgroups, one per (utterance, block of SEG_T segments): grid (B, P), so a short
 // batch still fills the chip; each writes its block's two correlation sums (double) to
-// part[b][p], which stoi_seg_sum adds up in block order (batch-independent); clean and denoised envelopes interleaved in LDS as (x, y) pairs (19 KB),
+// part[b][p], which stoi_seg_sum adds up in block order (batch-independent: SEG_T is fixed).
+// SEG_T = 256 (4 waves, 34 KB of LDS): per-kernel trace A/B at 4096 x 10 s, 3 rounds,
+// stoi_seg 0.970 vs 1.002 ms at 128 and the step 6.952 vs 7.001 ms; 384 and 512 lose 40 %
+// (profiles/r5_t).  Clean and denoised envelopes interleaved in LDS as (x, y) pairs,
 // so every clean/denoised pair of operations is one packed-FP32 instruction (v_pk_fma_f32 /
 // v_pk_add_f32 / v_pk_mul_f32: twice the v_fma_f32 rate on gfx950).  The per-lane row
 // statistics of the ESTOI time normalisation stay in registers (uniform-index writes from the
 // rolled band loop).
 #ifndef FSEM_SEG_T
-#define FSEM_SEG_T 128
+#define FSEM_SEG_T 256
 #endif
 #ifndef FSEM_SEG_OCC
 #define FSEM_SEG_OCC 3
@@ -598,44 +601,48 @@ __global__ void __launch_bounds__(SEG_T, FSEM_SEG_OCC)
       f2 nvar = {0.f, 0.f};  // sum over bands of rxy^2: the time normalisation's noise variance / 1e-24
 #pragma unroll 1
       for (int j = 0; j < NB; ++j) {
+        // the rows centred in place first: ||row||^2 = ||row - mu||^2 + N mu^2 (two non-negative
+        // terms, ~1 ulp) replaces the separate sum of squares, and the clipped row is
+        // fma(d, sc, sc mu) -- 30 packed instructions fewer per band
         f2 v[NSEG];
-        f2 s2 = {0.f, 0.f}, s1 = {0.f, 0.f};
+        f2 s1 = {0.f, 0.f};
 #pragma unroll
         for (int t = 0; t < NSEG; ++t) {
           v[t] = XY[j][tid + t];
-          s2 = __builtin_elementwise_fma(v[t], v[t], s2);
           s1 += v[t];
         }
+        const f2 mu = s1 * kInvN;
+        f2 dd = {0.f, 0.f};  // (sum dx^2, sum dy^2)
+#pragma unroll
+        for (int t = 0; t < NSEG; ++t) {
+          v[t] = v[t] - mu;
+          dd = __builtin_elementwise_fma(v[t], v[t], dd);
+        }
+        const f2 s2 = __builtin_elementwise_fma(mu * (float)NSEG, mu, dd);
         // equalize_clip (STOI.py:129-139).  Hardware sqrt / rcp / rsq (~1 ulp) instead of the
         // correctly rounded sequences: ~1e-7 relative per segment, far inside the tolerance.
         const float alpha = __builtin_amdgcn_sqrtf(s2.x) * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(s2.y) + 1e-9f);
-        const f2 sc = {kClip, alpha};  // (x * kClip, alpha * y): one packed multiply
-        // the clipped row by frame pairs (c[2u], c[2u + 1]), so its sum, centring and squares are
-        // packed operations too (even / odd partial sums)
+        const f2 sc = {kClip, alpha};  // (x * kClip, alpha * y)
+        const f2 smu = sc * mu;
         static_assert(NSEG % 2 == 0, "frame pairs");
         f2 c[NSEG / 2];
         f2 syc2 = {0.f, 0.f};
 #pragma unroll
         for (int u = 0; u < NSEG / 2; ++u) {
-          const f2 q0 = v[2 * u] * sc, q1 = v[2 * u + 1] * sc;
+          const f2 q0 = __builtin_elementwise_fma(v[2 * u], sc, smu), q1 = __builtin_elementwise_fma(v[2 * u + 1], sc, smu);
           c[u] = (f2){fminf(q0.y, q0.x), fminf(q1.y, q1.x)};
           syc2 += c[u];
         }
-        const f2 mu = s1 * kInvN;
         const float myc = (syc2.x + syc2.y) * kInvN;
         const f2 myc2 = {myc, myc};
-        f2 dd = {0.f, 0.f};  // (sum dx^2, sum dy^2)
         f2 dcc2 = {0.f, 0.f};
         float dxc = 0.f;
 #pragma unroll
         for (int u = 0; u < NSEG / 2; ++u) {
-          const f2 d0 = v[2 * u] - mu, d1 = v[2 * u + 1] - mu;
           const f2 dc = c[u] - myc2;
-          dd = __builtin_elementwise_fma(d0, d0, dd);
-          dd = __builtin_elementwise_fma(d1, d1, dd);
           dcc2 = __builtin_elementwise_fma(dc, dc, dcc2);
-          dxc = fmaf(d0.x, dc.x, dxc);
-          dxc = fmaf(d1.x, dc.y, dxc);
+          dxc = fmaf(v[2 * u].x, dc.x, dxc);
+          dxc = fmaf(v[2 * u + 1].x, dc.y, dxc);
         }
         const float dcc = dcc2.x + dcc2.y;
         // normalize() (STOI.py:113-119) centres, adds 1e-12 * randn and divides by the norm: in
