@@ -37,6 +37,7 @@ SIGNATURES = {
     "fsem_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "fsem_version": (ctypes.c_int, []),
     "fsem_build_id": (ctypes.c_char_p, []),
+    "fsem_host_buffer_mapped": (ctypes.c_int, [ctypes.c_void_p]),
     "fsem_resample_length": (_c_i64, [_c_i64, _c_i32, _c_i32]),
     "fsem_resample_f32": (ctypes.c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _c_i64, _c_i32, _c_i32, _vp]),
     "fsem_resample_rows_f32": (ctypes.c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_i64, _c_i32, _c_i32, _vp]),
@@ -177,7 +178,29 @@ def _host_slot(owner, n: int):
     if buf is None or buf.numel() < n:
         buf = torch.empty(max(n, 3 * 4096), dtype=torch.float32, pin_memory=True)
         tl.buf, tl.np, tl.ev = buf, buf.numpy(), torch.cuda.Event()
+        tl.mapped = bool(load().fsem_host_buffer_mapped(buf.data_ptr()))
     return buf[:n], tl.np[:n], tl.ev
+
+
+def mapped_host_slot(owner, n: int):
+    """`owner`'s pinned host buffer for this thread (as _host_slot) when the device may write it
+    directly (fsem_host_buffer_mapped: the same address on host and device), else None."""
+    pin, pin_np, ev = _host_slot(owner, n)
+    return (pin, pin_np, ev) if owner.__dict__["_fsem_tls"].mapped else None
+
+
+def list_from_host(owner, slot, K: int, B: int, keys: tuple, device):
+    """list_from_device for scores the kernels write straight into `slot` (mapped_host_slot):
+    no copy behind the kernels, only the event on the current stream."""
+    _, pin_np, ev = slot
+    ev.record(torch.cuda.current_stream(device))
+    owner._held_list = None
+    res, h = score_list_alloc(B, keys)
+    ev.synchronize()
+    host = pin_np[:K * B].reshape(K, B)
+    score_list_fill(h, 0, host, keys)
+    owner._held_list = h
+    return res, host
 
 
 def list_from_device(owner, t: torch.Tensor, keys: tuple):

@@ -1254,8 +1254,10 @@ int fsem::pesq::launch_front(const float *ref, const float *deg, int64_t batch, 
   int *rng = reinterpret_cast<int *>(static_cast<char *>(ws) + pesq::front_ppart_bytes(batch, length));
   int *pexp = rng;
   // shifts, worklist count, item queue and flags start at zero (the worklist itself is written
-  // before read)
-  if (hipMemsetAsync(rng, 0, sizeof(int) * ((size_t)(2 * batch) * g.nseg + 2 + 2 * (size_t)batch), st) != hipSuccess)
+  // before read); the size rounded up to 16 bytes (inside the 256-aligned region) so the runtime
+  // fills it with one kernel instead of an aligned body and a tail
+  if (hipMemsetAsync(rng, 0, align_up(sizeof(int) * ((size_t)(2 * batch) * g.nseg + 2 + 2 * (size_t)batch), 16), st) !=
+      hipSuccess)
     return FSEM_ELAUNCH;
 #define FSEM_FRONT(J, V, S)                                                                                      \
   hipLaunchKernelGGL((pesq::pesq_front<J, V, S>), dim3((unsigned)grid), dim3(pesq::PT), 0, st, ref, deg, batch,  \

@@ -948,7 +948,11 @@ extern "C" int fsem_pesq_stoi_f32(const float *ref, const float *deg, int64_t ba
   // batches (several waves per pair) start it as soon as the front end is done, beside
   // stoi_select / stoi_tob, since neither fills the chip.  Both only read what the front end wrote.
   const hipStream_t side = side_stream(st);
+#ifdef FSEM_BACK_EARLY
+  const bool early = true;
+#else
   const bool early = pesq::back_waves(batch, length) > 1;
+#endif
   rc = pesq::run_wb_front(ref, deg, batch, length, ld, lengths, ws, pesq_bytes, w.y10, g.y_ld, w.vad, g.v_ld, st);
   if (rc != FSEM_OK) return rc;
   if (early) {
@@ -992,7 +996,7 @@ extern "C" const char *fsem_strerror(int code) {
   }
 }
 
-extern "C" int fsem_version(void) { return 6; }  // 6: + fsem_build_id; 5: + fsem_time_align_utt_*; 4: + fsem_pre_emphasize_f32; 3: + fsem_time_align_*, fsem_pesq_distances_*
+extern "C" int fsem_version(void) { return 7; }  // 7: + fsem_host_buffer_mapped; 6: + fsem_build_id; 5: + fsem_time_align_utt_*; 4: + fsem_pre_emphasize_f32; 3: + fsem_time_align_*, fsem_pesq_distances_*
 
 // The build's content hash (_build.py passes -DFSEM_BUILD_ID); the marker prefix lets the host
 // layer read the id from the file without loading it (_build.library_build_id).
@@ -1001,3 +1005,15 @@ extern "C" int fsem_version(void) { return 6; }  // 6: + fsem_build_id; 5: + fse
 #endif
 static const char kBuildIdMarker[] = "FSEM_BUILD_ID:" FSEM_BUILD_ID;
 extern "C" const char *fsem_build_id(void) { return kBuildIdMarker + 14; }
+
+// The drop-in call's scores go straight into its pinned host buffer when the runtime maps that
+// buffer into the device address space at the same address (hipHostMalloc memory on ROCm).
+extern "C" int fsem_host_buffer_mapped(const void *p) {
+  if (!p) return 0;
+  void *d = nullptr;
+  if (hipHostGetDevicePointer(&d, const_cast<void *>(p), 0) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return d == p ? 1 : 0;
+}

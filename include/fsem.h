@@ -63,11 +63,15 @@ extern "C" {
 #define FSEM_ERATE -5         /* unsupported sample-rate pair (see resampling)      */
 
 const char *fsem_strerror(int code);
-int fsem_version(void);  /* 6: + fsem_build_id; 5: + fsem_time_align_utt_*; 4: + fsem_pre_emphasize_f32; 3: time alignment, distances */
+int fsem_version(void);  /* 7: + fsem_host_buffer_mapped; 6: + fsem_build_id; 5: + fsem_time_align_utt_*; 4: + fsem_pre_emphasize_f32; 3: time alignment, distances */
 /* Content hash (16 hex digits) of the sources, headers and compile flags this library was built
  * from (fast_speech_enhancement_metrics_amd/_build.py source_hash); the host layer refuses a
  * library whose id differs from its own tree's.  "unknown" for builds outside _build.py. */
 const char *fsem_build_id(void);
+/* 1 when the page-locked host buffer p is mapped into the device address space at the same
+ * address (so an entry may write its scores straight into it), else 0.  Host-side query, no
+ * kernel. */
+int fsem_host_buffer_mapped(const void *p);
 
 /* ---------------------------------------------------------------- resampling
  * torchaudio.transforms.Resample(orig, new) (sinc_interp_hann, width 6,

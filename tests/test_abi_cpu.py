@@ -41,6 +41,7 @@ def test_version_and_errors(lib):
     assert lib.fsem_version() >= 1
     assert lib.fsem_strerror(0) == b"ok"
     assert b"workspace" in lib.fsem_strerror(-2)
+    assert lib.fsem_host_buffer_mapped(None) == 0  # (no runtime call for a null buffer)
 
 
 @pytest.mark.parametrize("L", [160000, 48000, 40077, 5376, 511, 255, 100])

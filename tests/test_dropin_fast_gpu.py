@@ -1,7 +1,8 @@
 """The drop-in call's fast path (joint.py PESQ_STOI._fast_call: launch first, dicts built and the
 previous call's list released while the GPU computes): the same list as the generic path,
 bitwise; inputs it does not cover take the generic path; the reference's exceptions and warning
-stay; the previous list's dicts are held until the next call and then released."""
+stay; the previous list's dicts are held until the next call and then released; the scores land
+in the thread's mapped pinned buffer directly (no device copy), the same as through a copy."""
 import gc
 import sys
 import warnings
@@ -101,3 +102,22 @@ def test_no_stoi_segment_warns_like_reference():
             res = call()
         assert any("non-silent" in str(x.message) for x in w)
         assert all(d["STOI"] != d["STOI"] and d["PESQ"] == d["PESQ"] for d in res)
+
+
+def test_scores_written_into_mapped_host_buffer(pairs):
+    """fsem_host_buffer_mapped holds for torch's pinned memory on this runtime, so the fast path's
+    kernels write the scores straight into the thread's pinned buffer: the buffer holds them after
+    the call, and they equal the device-buffer + copy form (host_scores = False) bitwise."""
+    from fast_speech_enhancement_metrics_amd import PESQ_STOI, _native
+    c, n = pairs
+    B = c.shape[0]
+    m = PESQ_STOI(16000, use_gpu=True)
+    assert _native.mapped_host_slot(m, 3 * B) is not None
+    res = m(c, n)
+    host = m.__dict__["_fsem_tls"].np[:3 * B].reshape(3, B)
+    np.testing.assert_array_equal(host[0], np.array([d["PESQ"] for d in res], np.float32))
+    np.testing.assert_array_equal(host[2], np.array([d["ESTOI"] for d in res], np.float32))
+    cp = PESQ_STOI(16000, use_gpu=True)
+    cp.host_scores = False
+    assert cp(c, n) == res
+    assert not _native.load().fsem_host_buffer_mapped(None)

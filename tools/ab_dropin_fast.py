@@ -1,6 +1,8 @@
 """Interleaved A/B of the drop-in call PESQ_STOI(16000, use_gpu=True)(clean, noisy) -> list of
 dicts, timed as bench.py times it (wall clock over back-to-back calls, the result dropped each
-time): the fast path (joint.py _fast_call) against the generic path, in one process.
+time): the fast path (joint.py _fast_call) against the generic path, and the fast path with its
+scores copied from a device buffer (host_scores = False) against written straight into mapped
+pinned memory, in one process.
 
     python tools/ab_dropin_fast.py [--batch 4096] [--steps 20] [--rounds 6]
 """
@@ -26,13 +28,16 @@ c, n, _ = speech_like_pairs(a.batch, a.length, 16000, seed=42, device="cuda")
 fast = PESQ_STOI(16000, use_gpu=True)
 slow = PESQ_STOI(16000, use_gpu=True)
 slow._fast_ok = lambda *x: False
-for m in (fast, slow):
+copy = PESQ_STOI(16000, use_gpu=True)
+copy.host_scores = False
+for m in (fast, slow, copy):
     for _ in range(5):
         m(c, n)
 torch.cuda.synchronize()
-t = {"fast": [], "generic": []}
+t = {"fast": [], "generic": [], "fast_copy": []}
+order = [("fast", fast), ("generic", slow), ("fast_copy", copy)]
 for r in range(a.rounds):
-    for name, m in ((("fast", fast), ("generic", slow)) if r % 2 == 0 else (("generic", slow), ("fast", fast))):
+    for name, m in (order if r % 2 == 0 else order[::-1]):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(a.steps):
@@ -42,4 +47,4 @@ for r in range(a.rounds):
 for name, v in t.items():
     print(f"{name}: median {statistics.median(v):.4f} ms per call  min {min(v):.4f}  max {max(v):.4f}  "
           f"({a.batch / statistics.median(v) * 1e3:,.0f} utt/s)")
-print("equal lists:", fast(c, n) == slow(c, n))
+print("equal lists:", fast(c, n) == slow(c, n) == copy(c, n))
