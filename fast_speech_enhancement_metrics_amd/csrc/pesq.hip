@@ -898,11 +898,7 @@ __global__ void __launch_bounds__(PT, 2)
       else
         acc = iir_pass2_masked<false>(w4, z, own_lo, own_hi, lim, t_lane, L, xm1, xm1 - xm2);
       // per-wave partials (no workgroup barrier); pesq_power_sum adds them in a fixed order
-#ifdef FSEM_WAVE_SUM_SHFL
-      const float tot = wave_sum(acc);
-#else
       const float tot = wave_sum_dpp(acc);
-#endif
       if (lane == 0) ppart[(it.s * nseg + g) * 4 + wave] = tot * (kBpGain * kBpGain);
     }
     lds_barrier();

@@ -391,18 +391,11 @@ __global__ void __launch_bounds__(64 * TOB_WAVES)
   for (int u = 0; u < NBW; ++u) {
     const int j = wave + TOB_WAVES * u;
     if (j < nblk) {  // uniform
-#ifdef FSEM_TOB_ADDTID
-      lds_store_lanes(&blk[0][j][0], w_lo * g[u][0] + w_hi * g[u][1]);
-      lds_store_lanes(&blk[0][j][64], w_lo2 * g[u][2] + w_hi2 * g[u][3]);
-      lds_store_lanes(&blk[1][j][0], w_lo * g[u][4] + w_hi * g[u][5]);
-      lds_store_lanes(&blk[1][j][64], w_lo2 * g[u][6] + w_hi2 * g[u][7]);
-#else
       // plain lane-ordered stores (one address VGPR, immediate offsets): no M0 juggling
       blk[0][j][lane] = w_lo * g[u][0] + w_hi * g[u][1];
       blk[0][j][64 + lane] = w_lo2 * g[u][2] + w_hi2 * g[u][3];
       blk[1][j][lane] = w_lo * g[u][4] + w_hi * g[u][5];
       blk[1][j][64 + lane] = w_lo2 * g[u][6] + w_hi2 * g[u][7];
-#endif
     }
   }
   lds_stores_done();  // other waves read these blocks
@@ -488,13 +481,6 @@ __global__ void __launch_bounds__(64 * TOB_WAVES)
       pa[r] = pp.x;
       pb[r] = pp.y;
     }
-#ifdef FSEM_TOB_ADDTID
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      lds_store_lanes(pbuf + 64 * r, pa[r]);
-      lds_store_lanes(pbuf + 256 + 64 * r, pb[r]);
-    }
-#else
     // plain lane-ordered stores: one address VGPR for the kernel, immediate offsets (paired
     // ds_write2st64_b32) -- no M0 save / set / hazard nop / restore per store (4 SALU each, 32
     // per transform: the kernel is issue bound, SQ_INSTS_SALU 45 % of its VALU count)
@@ -503,7 +489,6 @@ __global__ void __launch_bounds__(64 * TOB_WAVES)
       pbuf[64 * r + lane] = pa[r];
       pbuf[256 + 64 * r + lane] = pb[r];
     }
-#endif
     wave_lds_fence();
     {
       // band sums: one <=9-bin piece per lane (lanes of piece set 0: frame a, set 1: frame b),
