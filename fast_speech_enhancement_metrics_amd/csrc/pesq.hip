@@ -1245,7 +1245,14 @@ int fsem::pesq::launch_front(const float *ref, const float *deg, int64_t batch, 
     const int v = e ? atoi(e) : 0;
     return (v >= 1 && v <= 2) ? v : 2;
   }();
-  const int64_t grid = std::min<int64_t>(nitems, (int64_t)ncu * wgs_per_cu);
+  // FSEM_FRONT_CUS (diagnostics only: tools/ab_overlap.py's partitioned grid) caps the CUs the
+  // persistent grid is sized for, leaving the rest to kernels on other streams
+  static const int front_cus = [] {
+    const char *e = getenv("FSEM_FRONT_CUS");
+    return e ? atoi(e) : 0;
+  }();
+  const int64_t cus = (front_cus > 0 && front_cus < ncu) ? front_cus : ncu;
+  const int64_t grid = std::min<int64_t>(nitems, cus * wgs_per_cu);
   float *ppart = static_cast<float *>(ws);
   int *rng = reinterpret_cast<int *>(static_cast<char *>(ws) + pesq::front_ppart_bytes(batch, length));
   int *pexp = rng;
