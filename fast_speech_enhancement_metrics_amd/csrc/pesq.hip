@@ -68,15 +68,11 @@ constexpr int CH = FSEM_PESQ_CH;  // 52 samples per lane (stride 208 B: conflict
 constexpr int TILE = PT * CH;     // 13312
 constexpr int WARM = 768;
 constexpr int NS = 12;            // scan states: 10 band-pass (5 sections) + 2 pre-emphasis
-// floats per lane in the scan buffer: 12 (the states as three 16-byte words: ds_read_b128 /
+// floats per lane in the scan buffer: 12, the states as three 16-byte words (ds_read_b128 /
 // ds_write_b128, conflict-free at a 48-byte stride -- lanes l, l + 16 share banks, and the
 // b128 lane groups hold distinct l mod 16; one LDS round trip per scan level instead of six
-// ds_read2_b32 waited for one by one); 13 (odd, b32 accesses) with FSEM_SCAN_B32
-#ifdef FSEM_SCAN_B32
-constexpr int SCAN_LD = 13;
-#else
+// ds_read2_b32 waited for one by one)
 constexpr int SCAN_LD = 12;
-#endif
 // exchange buffer: 4 waves x 512 complex for the FFTs, the resampler's per-wave staging slices
 // (4 x 960 floats, joint entry), or the two buffers of the double-buffered chunk scan.  Scan
 // buffer A keeps wave w's states inside wave w's own staging slice (960 w + 13 lane: no wave
@@ -788,34 +784,19 @@ __global__ void __launch_bounds__(PT, 2)
     auto scan_at = [&](bool in_b, int t) {
       return in_b ? xbuf + SCAN_B0 + t * SCAN_LD : xbuf + SCAN_A_WAVE * (t >> 6) + (t & 63) * SCAN_LD;
     };
-    // the 12 states of a lane as float4 words (SCAN_LD = 12) or single floats (13)
+    // the 12 states of a lane as three float4 words
     auto put_states = [&](float *dst) {
-      if (SCAN_LD == 12) {
-        float4 *d4 = reinterpret_cast<float4 *>(dst);
-        d4[0] = make_float4(e[0], e[1], e[2], e[3]);
-        d4[1] = make_float4(e[4], e[5], e[6], e[7]);
-        d4[2] = make_float4(e[8], e[9], e[10], e[11]);
-      } else {
-#pragma unroll
-        for (int i = 0; i < NS; ++i) dst[i] = e[i];
-      }
+      float4 *d4 = reinterpret_cast<float4 *>(dst);
+      d4[0] = make_float4(e[0], e[1], e[2], e[3]);
+      d4[1] = make_float4(e[4], e[5], e[6], e[7]);
+      d4[2] = make_float4(e[8], e[9], e[10], e[11]);
     };
-#ifdef FSEM_SCAN_KEEP_MUL
-    constexpr bool KEEP_MUL = true;
-#else
-    constexpr bool KEEP_MUL = false;
-#endif
-    auto get_states = [&](const float *src, float keep, float q[NS]) {
-      if (SCAN_LD == 12) {
-        const float4 *s4 = reinterpret_cast<const float4 *>(src);
-        const float4 a = s4[0], b = s4[1], c = s4[2];
-        const float v[NS] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w};
+    auto get_states = [&](const float *src, float q[NS]) {
+      const float4 *s4 = reinterpret_cast<const float4 *>(src);
+      const float4 a = s4[0], b = s4[1], c = s4[2];
+      const float v[NS] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w};
 #pragma unroll
-        for (int i = 0; i < NS; ++i) q[i] = KEEP_MUL ? v[i] * keep : v[i];
-      } else {
-#pragma unroll
-        for (int i = 0; i < NS; ++i) q[i] = src[i] * keep;
-      }
+      for (int i = 0; i < NS; ++i) q[i] = v[i];
     };
     put_states(scan_at(false, tid));
     lds_barrier();
@@ -824,10 +805,8 @@ __global__ void __launch_bounds__(PT, 2)
       const int d = 1 << lv;
       float q[NS];
       // lanes without a chunk d back read the zero row (an address select instead of 12
-      // multiplications by a 0/1 flag; FSEM_SCAN_KEEP_MUL: the multiplications)
-      const float *src = KEEP_MUL ? scan_at(lv & 1, max(tid - d, 0)) : (tid >= d ? scan_at(lv & 1, tid - d) : zrow);
-      const float keep = (tid >= d) ? 1.f : 0.f;
-      get_states(src, keep, q);
+      // multiplications by a 0/1 flag)
+      get_states(tid >= d ? scan_at(lv & 1, tid - d) : zrow, q);
 #pragma unroll
       for (int i = 0; i < NBP; ++i) {
         float acc = e[i];
@@ -848,9 +827,7 @@ __global__ void __launch_bounds__(PT, 2)
     // start state of chunk j = inclusive prefix of chunk j-1 (level 3 wrote buffer A)
     float z[NS];
     {
-      const float *src = KEEP_MUL ? scan_at(false, max(tid - 1, 0)) : (tid >= 1 ? scan_at(false, tid - 1) : zrow);
-      const float keep = (tid >= 1) ? 1.f : 0.f;
-      get_states(src, keep, z);
+      get_states(tid >= 1 ? scan_at(false, tid - 1) : zrow, z);
       // pre-emphasis: scan basis (u, v) -> direct-form states (y[n-1], y[n-2]) (gen_tables.py)
       const float u = z[NBP], v = z[NBP + 1];
       z[NBP] = fmaf(kPreToY[0][0], u, kPreToY[0][1] * v);

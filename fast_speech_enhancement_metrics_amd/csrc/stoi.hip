@@ -31,7 +31,10 @@ namespace stoi {
 constexpr int NB = 15;     // one-third octave bands
 constexpr int NSEG = 30;   // frames per segment
 constexpr int VF = 64;     // VAD frames per workgroup
-constexpr int TF = 32;     // STFT frames per workgroup
+#ifndef FSEM_TOB_TF
+#define FSEM_TOB_TF 32
+#endif
+constexpr int TF = FSEM_TOB_TF;  // STFT frames per workgroup
 constexpr float kClip = 1.0f + 5.62341325190349f;  // 1 + 10^(-beta/20), beta = -15 (STOI.py:136-137)
 
 // Per-row lengths: row b holds lens[b] input samples (clamped to [0, ncap]) when lens is
@@ -933,11 +936,7 @@ extern "C" int fsem_pesq_stoi_f32(const float *ref, const float *deg, int64_t ba
   // batches (several waves per pair) start it as soon as the front end is done, beside
   // stoi_select / stoi_tob, since neither fills the chip.  Both only read what the front end wrote.
   const hipStream_t side = side_stream(st);
-#ifdef FSEM_BACK_EARLY
-  const bool early = true;
-#else
   const bool early = pesq::back_waves(batch, length) > 1;
-#endif
   rc = pesq::run_wb_front(ref, deg, batch, length, ld, lengths, ws, pesq_bytes, w.y10, g.y_ld, w.vad, g.v_ld, st);
   if (rc != FSEM_OK) return rc;
   if (early) {
