@@ -128,7 +128,10 @@ class PESQ_STOI(BaseMetric):
         dev = noisy.device.index
         return clean.device.index == dev and dev == torch.cuda.current_device()
 
-    def _fast_call(self, clean: torch.Tensor, noisy: torch.Tensor) -> list[dict[str, float]]:
+    def _fast_call(self, clean: torch.Tensor, noisy: torch.Tensor, device_scores: bool = False):
+        """The list of dicts; with ``device_scores`` also the [B, 3] float32 scores on the device
+        (for ``call_with_scores``: the scores then land in a device buffer and reach the host by
+        one copy)."""
         lib = _native.load()
         B, L = noisy.shape
         dev = noisy.device
@@ -138,7 +141,7 @@ class PESQ_STOI(BaseMetric):
             wsb = self._ws_bytes[(B, L)] = lib.fsem_pesq_stoi_workspace_bytes(B, L)
         # the scores go straight into the thread's pinned host buffer when the device maps it
         # (no device->host copy behind the kernels: ~20 us of the step's idle tail)
-        slot = _native.mapped_host_slot(self, 3 * B) if self.host_scores else None
+        slot = _native.mapped_host_slot(self, 3 * B) if self.host_scores and not device_scores else None
         if slot is not None:
             o = slot[0].data_ptr()
             outs = (o, o + 4 * B, o + 8 * B)
@@ -157,7 +160,7 @@ class PESQ_STOI(BaseMetric):
             res, _ = _native.list_from_device(self, out, _KEYS)
         if res[0]["STOI"] != res[0]["STOI"] and all(d["STOI"] != d["STOI"] for d in res):  # STOI.py:162-165
             warnings.warn("Not enough non-silent frames. Please check your sound files", RuntimeWarning, stacklevel=3)
-        return res
+        return (res, out.t()) if device_scores else res
 
     # Rows per chunk when the drop-in call splits a GPU batch into consecutive engine calls
     # (below); 0: one call.  The chunks existed to overlap building chunk k's dicts with chunk
@@ -243,6 +246,8 @@ class PESQ_STOI(BaseMetric):
             res = self(clean_speech, denoised_speech, lengths)
             t = torch.tensor([[d["PESQ"], d["STOI"], d["ESTOI"]] for d in res], dtype=torch.float32)
             return res, t.to(self.device)
+        if lengths is None and self._fast_ok(clean_speech, denoised_speech):
+            return self._fast_call(clean_speech, denoised_speech, device_scores=True)
         clean_speech, denoised_speech, lengths = self.split_ragged(clean_speech, denoised_speech, lengths)
         clean_speech, denoised_speech = self.prepare_inputs(clean_speech, denoised_speech, lengths)
         assert clean_speech is not None

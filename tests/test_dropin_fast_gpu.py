@@ -121,3 +121,19 @@ def test_scores_written_into_mapped_host_buffer(pairs):
     cp.host_scores = False
     assert cp(c, n) == res
     assert not _native.load().fsem_host_buffer_mapped(None)
+
+
+def test_call_with_scores_fast_path(pairs):
+    """call_with_scores (the bench's multi-rank step: the list plus the [B, 3] device scores for the
+    all-gather) takes the fast path too: the same list and scores as the generic path, bitwise."""
+    from fast_speech_enhancement_metrics_amd import PESQ_STOI
+    c, n = pairs
+    m = PESQ_STOI(16000, use_gpu=True)
+    res, t = m.call_with_scores(c, n)
+    m._fast_ok = lambda *a: False
+    res_g, t_g = m.call_with_scores(c, n)
+    del m._fast_ok
+    assert res == res_g
+    assert t.shape == (c.shape[0], 3) and t.is_cuda and t.dtype == torch.float32
+    np.testing.assert_array_equal(t.cpu().numpy(), t_g.cpu().numpy())
+    np.testing.assert_array_equal(t[:, 0].cpu().numpy(), np.array([d["PESQ"] for d in res], np.float32))
