@@ -137,3 +137,18 @@ def test_call_with_scores_fast_path(pairs):
     assert t.shape == (c.shape[0], 3) and t.is_cuda and t.dtype == torch.float32
     np.testing.assert_array_equal(t.cpu().numpy(), t_g.cpu().numpy())
     np.testing.assert_array_equal(t[:, 0].cpu().numpy(), np.array([d["PESQ"] for d in res], np.float32))
+
+
+@pytest.mark.parametrize("B", [1, 3, 65])
+def test_fast_path_small_and_odd_batches(B):
+    """The fast path at batch sizes that take the back end's multi-wave forms (B <= 2 per CU) and
+    an odd count: the same dicts as the generic path, bitwise, the mapped buffer reused across
+    sizes."""
+    from fast_speech_enhancement_metrics_amd import PESQ_STOI
+    from fast_speech_enhancement_metrics_amd.synthetic import speech_like_pairs
+    c, n, _ = speech_like_pairs(B, 32000, 16000, seed=80 + B, device="cuda")
+    m = PESQ_STOI(16000, use_gpu=True)
+    assert m._fast_ok(c, n)
+    fast = m(c, n)
+    assert len(fast) == B and fast == _generic(m, c, n)
+    assert m(c[:1], n[:1]) == fast[:1]  # a smaller call after a larger one on the same buffer
