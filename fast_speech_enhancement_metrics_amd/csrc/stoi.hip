@@ -563,15 +563,19 @@ __global__ void __launch_bounds__(SEG_T, FSEM_SEG_OCC)
   constexpr float kInvN = 1.f / NSEG;
   {
     const int nf = min(W, T - m0);
-    // all 2 x 15 x 158 loads of the pass in flight at once (one latency round), then the stores
+    // all 2 x 15 x W loads of the pass in flight at once (one latency round), then the stores.
+    // Frame indices clamped to the block's last frame instead of predicated loads (no branch per
+    // load): the slots past nf hold copies no segment of this block reads (segment m = m0 + tid <
+    // S reads frames tid .. tid + 29 < nf)
     {
       f2 va[NB], vb[NB];
       const int t2 = tid + SEG_T;
+      const int ia = min(tid, nf - 1), ib = min(t2, nf - 1);
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
         const float *xr = xc + j * tmax + m0, *dr = xd + j * tmax + m0;
-        va[j] = (tid < nf) ? (f2){xr[tid], dr[tid]} : (f2){0.f, 0.f};
-        vb[j] = (t2 < nf) ? (f2){xr[t2], dr[t2]} : (f2){0.f, 0.f};
+        va[j] = (f2){xr[ia], dr[ia]};
+        vb[j] = (f2){xr[ib], dr[ib]};
       }
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
