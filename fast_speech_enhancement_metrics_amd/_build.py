@@ -39,8 +39,13 @@ HEADERS = ["fsem_common.h", "fsem_fft.h", "fsem_internal.h", "fsem_pesq.h", "fse
            "fsem_vad.h"]
 HEADER_ABI = os.path.join(PKG, "..", "include", "fsem.h")
 ARCH = os.environ.get("FSEM_OFFLOAD_ARCH", "gfx950")
-BASE_FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-Wno-unused-result"]
+# code-generation flags; the target (--offload-arch=ARCH) is added at build time and recorded in
+# the library on its own (FSEM_BUILD_ARCH): a library built for another target is refused at
+# load, never silently rebuilt (_native._check_build_id)
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wno-unused-result"]
+BASE_FLAGS = FLAGS + [f"--offload-arch={ARCH}"]
 _ID_MARKER = b"FSEM_BUILD_ID:"
+_ARCH_MARKER = b"FSEM_BUILD_ARCH:"
 # the drop-in call's list-of-dicts builder (host C, CPython API; csrc/score_list.c)
 SCORE_LIST_SRC = os.path.join(CSRC, "score_list.c")
 SCORE_LIST = os.path.join(LIBDIR, "_score_list" + sysconfig.get_config_var("EXT_SUFFIX"))
@@ -60,14 +65,15 @@ def deps() -> list:
 
 def source_hash() -> str:
     """Content hash of the sources, the headers (csrc/*.h, fsem_tables.inc, include/fsem.h) and
-    the compile flags (BASE_FLAGS, SOURCE_FLAGS): the library's build id (fsem_build_id())."""
+    the code-generation flags (FLAGS, SOURCE_FLAGS; not the target, see library_build_arch): the
+    library's build id (fsem_build_id())."""
     h = hashlib.sha256()
     for d in deps():
         h.update(os.path.basename(d).encode() + b"\0")
         with open(d, "rb") as f:
             h.update(f.read())
         h.update(b"\0")
-    h.update(repr((BASE_FLAGS, sorted(SOURCE_FLAGS.items()))).encode())
+    h.update(repr((FLAGS, sorted(SOURCE_FLAGS.items()))).encode())
     return h.hexdigest()[:16]
 
 
@@ -82,11 +88,22 @@ def library_build_id(path: str = LIB):
     return m.group(1).decode() if m else None
 
 
+def library_build_arch(path: str = LIB):
+    """The offload target a built library was compiled for (read from the file), or None."""
+    try:
+        with open(path, "rb") as f:
+            data = f.read()
+    except OSError:
+        return None
+    m = re.search(re.escape(_ARCH_MARKER) + rb"([0-9a-z_:+-]+)\0", data)
+    return m.group(1).decode() if m else None
+
+
 def _stale() -> bool:
     """True when libfsem.so is missing or was built from other sources or flags than the tree's
     (content hash: an edited header or a changed SOURCE_FLAGS entry rebuilds; a touched file
-    whose content is unchanged does not)."""
-    return library_build_id(LIB) != source_hash()
+    whose content is unchanged does not), or for another target than ARCH."""
+    return library_build_id(LIB) != source_hash() or library_build_arch(LIB) != ARCH
 
 
 def build(force: bool = False, verbose: bool = False, stamps: bool = False) -> str:
@@ -98,7 +115,7 @@ def build(force: bool = False, verbose: bool = False, stamps: bool = False) -> s
     # each other's objects; the finished library replaces the old one atomically
     objdir = os.path.join(LIBDIR, f"obj{'_stamps' if stamps else ''}.{os.getpid()}")
     os.makedirs(objdir, exist_ok=True)
-    base = [_hipcc()] + BASE_FLAGS + [f'-DFSEM_BUILD_ID="{source_hash()}"']
+    base = [_hipcc()] + BASE_FLAGS + [f'-DFSEM_BUILD_ID="{source_hash()}"', f'-DFSEM_BUILD_ARCH="{ARCH}"']
     if stamps:
         base.append("-DFSEM_STAMPS")
     objs = []

@@ -167,26 +167,41 @@ def score_list_fill(handle, offset: int, scores, keys: tuple) -> None:
     mod.score_list_fill(handle, offset, scores, keys)
 
 
-def _host_slot(owner, n: int):
-    """(pinned float32 host buffer of >= n elements, its numpy view, an event) of `owner` (a metric)
-    and this host thread, kept across calls: a drop-in call waits for its copy before returning,
-    so the next call on the thread may reuse them."""
+def _host_slot(owner, n: int, device):
+    """(pinned float32 host buffer of >= n elements, its numpy view, an event) of `owner` (a metric),
+    this host thread and `device`, kept across calls: a drop-in call waits for its copy before
+    returning, so the next call on the thread may reuse them.  Keyed by device: an event belongs
+    to the device of its first record, and whether the device maps the buffer
+    (fsem_host_buffer_mapped) is a property of that device."""
     tl = owner.__dict__.get("_fsem_tls")
     if tl is None:
         tl = owner.__dict__.setdefault("_fsem_tls", threading.local())
-    buf = getattr(tl, "buf", None)
-    if buf is None or buf.numel() < n:
+    slots = getattr(tl, "slots", None)
+    if slots is None:
+        slots = tl.slots = {}
+    idx = torch.device(device).index
+    if idx is None:
+        idx = torch.cuda.current_device()
+    slot = slots.get(idx)
+    if slot is None or slot[0].numel() < n:
         buf = torch.empty(max(n, 3 * 4096), dtype=torch.float32, pin_memory=True)
-        tl.buf, tl.np, tl.ev = buf, buf.numpy(), torch.cuda.Event()
-        tl.mapped = bool(load().fsem_host_buffer_mapped(buf.data_ptr()))
-    return buf[:n], tl.np[:n], tl.ev
+        with torch.cuda.device(idx):
+            mapped = bool(load().fsem_host_buffer_mapped(buf.data_ptr()))
+            ev = torch.cuda.Event()
+        slot = slots[idx] = (buf, buf.numpy(), ev, mapped)
+    buf, buf_np, ev, _ = slot
+    return buf[:n], buf_np[:n], ev
 
 
-def mapped_host_slot(owner, n: int):
-    """`owner`'s pinned host buffer for this thread (as _host_slot) when the device may write it
-    directly (fsem_host_buffer_mapped: the same address on host and device), else None."""
-    pin, pin_np, ev = _host_slot(owner, n)
-    return (pin, pin_np, ev) if owner.__dict__["_fsem_tls"].mapped else None
+def mapped_host_slot(owner, n: int, device=None):
+    """`owner`'s pinned host buffer for this thread and `device` (as _host_slot) when that device
+    may write it directly (fsem_host_buffer_mapped: the same address on host and device), else
+    None."""
+    if device is None:
+        device = torch.device("cuda", torch.cuda.current_device())
+    pin, pin_np, ev = _host_slot(owner, n, device)
+    idx = torch.device(device).index
+    return (pin, pin_np, ev) if owner.__dict__["_fsem_tls"].slots[idx][3] else None
 
 
 def list_from_host(owner, slot, K: int, B: int, keys: tuple, device):
@@ -203,6 +218,15 @@ def list_from_host(owner, slot, K: int, B: int, keys: tuple, device):
     return res, host
 
 
+def release(owner) -> None:
+    """Drop what a metric keeps between drop-in calls: the last result list's fill handle and this
+    host thread's pinned score buffers (BaseMetric.release)."""
+    owner.__dict__.pop("_held_list", None)
+    tl = owner.__dict__.get("_fsem_tls")
+    if tl is not None and getattr(tl, "slots", None):
+        tl.slots = {}
+
+
 def list_from_device(owner, t: torch.Tensor, keys: tuple):
     """The drop-in call's result list from [K, B] float32 scores on the GPU, (list, host scores
     [K, B] numpy).  Enqueues the scores' copy into pinned host memory behind the kernels on the
@@ -212,7 +236,7 @@ def list_from_device(owner, t: torch.Tensor, keys: tuple):
     caller drops is then freed during the next call's kernels instead of between two calls, when
     the GPU would wait for it (4096 dicts: ~0.1-0.2 ms of deallocation)."""
     K, B = t.shape
-    pin, pin_np, ev = _host_slot(owner, K * B)
+    pin, pin_np, ev = _host_slot(owner, K * B, t.device)
     pin.view(K, B).copy_(t, non_blocking=True)
     ev.record(torch.cuda.current_stream(t.device))
     owner._held_list = None  # the previous call's list, released while the GPU computes
@@ -235,18 +259,31 @@ class NativeError(RuntimeError):
 
 def _check_build_id() -> None:
     """The in-tree library must be the build of this tree's sources and flags (_build.source_hash,
-    embedded as fsem_build_id()): a stale library is rebuilt where hipcc is available, else the
-    load fails loudly -- no kernel runs from a binary the committed sources did not produce.
-    FSEM_LIB (a library variant chosen explicitly, tools/ab_*.py) is not checked."""
+    embedded as fsem_build_id()) for this process's target (_build.ARCH, FSEM_OFFLOAD_ARCH):
+
+    * built for another target -> ImportError, never a rebuild (a gfx942 build loaded by a
+      process that did not set FSEM_OFFLOAD_ARCH is not silently replaced by a gfx950 one);
+    * stale (other sources or flags) -> ImportError, unless FSEM_AUTOBUILD=1 opts in to a rebuild
+      with hipcc (so the ranks of a multi-process job do not each run hipcc at import);
+
+    no kernel runs from a binary the committed sources did not produce.  FSEM_LIB (a library
+    variant chosen explicitly, tools/ab_*.py) is not checked."""
     if LIB_PATH != _DEFAULT_LIB:
         return
     from . import _build
     if not all(os.path.exists(d) for d in _build.deps()):
         return  # no source tree next to the package (nothing to compare with)
+    arch = _build.library_build_arch(LIB_PATH)
+    if arch != _build.ARCH:
+        raise ImportError(f"fsem HIP engine {LIB_PATH} was built for {arch}, this process targets {_build.ARCH} "
+                          "(FSEM_OFFLOAD_ARCH): rebuild it with `python -m fast_speech_enhancement_metrics_amd._build`")
     want = _build.source_hash()
     have = _build.library_build_id(LIB_PATH)
     if have == want:
         return
+    if os.environ.get("FSEM_AUTOBUILD") != "1":
+        raise ImportError(f"fsem HIP engine {LIB_PATH} is stale (build id {have}, sources {want}): rebuild it with "
+                          "`python -m fast_speech_enhancement_metrics_amd._build` (or set FSEM_AUTOBUILD=1)")
     try:
         _build.build(force=True)
     except Exception as exc:  # noqa: BLE001 -- any build failure: refuse the stale binary

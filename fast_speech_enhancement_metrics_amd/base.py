@@ -40,6 +40,30 @@ class BaseMetric(ABC):
             if self.devices is not None:  # (one listed device: its own thread and stream alike)
                 self._fanout = FanOut(self.devices)
 
+    # ---- what a GPU metric keeps between calls (the drop-in call's pinned score buffers and
+    # event per host thread and device, the last result list's fill handle, the fan-out's
+    # threads and streams) is process state: it is dropped when a metric is copied or pickled
+    # (the reference's BaseMetric is a plain object; copies of it stay possible) and rebuilt on use.
+    _TRANSIENT = ("_fsem_tls", "_held_list", "_fanout")
+
+    def release(self) -> None:
+        """Free the pinned score buffers and the last result list this metric keeps for its next
+        call (they are rebuilt on the next call)."""
+        _native.release(self)
+
+    def __getstate__(self):
+        state = self.__dict__.copy()
+        for k in self._TRANSIENT:
+            state.pop(k, None)
+        return state
+
+    def __setstate__(self, state):
+        self.__dict__.update(state)
+        self._fanout = None
+        if self.devices is not None:
+            from .multidevice import FanOut
+            self._fanout = FanOut(self.devices)
+
     def home_device(self):
         """Where results live: the first listed device of a multi-device metric, else ``.device``."""
         return self.device if self.devices is None else self.devices[0]

@@ -27,6 +27,19 @@
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
 
+/* The in-place fill relies on the refcount semantics of GIL builds of CPython up to 3.13: a
+ * float whose count is 2 is referenced by its dict and the handle only.  Free-threaded builds
+ * (Py_GIL_DISABLED: biased, shared counts) and later versions (deferred reference counting) may
+ * report other counts, so there every value goes in through PyDict_SetItem -- the same list, a
+ * few ns more per value.  `inplace_fill` also switches it off at run time (set_inplace: the
+ * tests compare the two forms). */
+#if !defined(Py_GIL_DISABLED) && PY_VERSION_HEX < 0x030E0000
+#define FSEM_INPLACE_FLOATS 1
+#else
+#define FSEM_INPLACE_FLOATS 0
+#endif
+static int inplace_fill = FSEM_INPLACE_FLOATS;
+
 /* keys: a non-empty tuple of str (hashes cached once); returns K or -1 with an exception set */
 static Py_ssize_t check_keys(PyObject *keys) {
   const Py_ssize_t K = PyTuple_GET_SIZE(keys);
@@ -201,11 +214,15 @@ static PyObject *score_list_fill(PyObject *self, PyObject *args) {
     for (Py_ssize_t k = 0; k < K; ++k) {
       const double x = f64 ? w[k * B + b] : (double)v[k * B + b];
       PyObject *f = p->f[(off + b) * K + k];
-      if (Py_REFCNT(f) == 2) {
+#if FSEM_INPLACE_FLOATS
+      if (inplace_fill && Py_REFCNT(f) == 2) {
         /* referenced by its dict and the handle only: not yet visible to anyone else */
         ((PyFloatObject *)f)->ob_fval = x;
         continue;
       }
+#else
+      (void)f;
+#endif
       /* replaced or shared since the allocation: a new float through the dict API */
       PyObject *d = PyList_GET_ITEM(p->lst, off + b);
       if (!PyDict_Check(d)) {
@@ -226,7 +243,19 @@ done:
   return ret;
 }
 
+/* set_inplace(flag) -> previous flag: the in-place fill on (where compiled in) or off */
+static PyObject *set_inplace(PyObject *self, PyObject *arg) {
+  (void)self;
+  const int on = PyObject_IsTrue(arg);
+  if (on < 0) return NULL;
+  const int prev = inplace_fill;
+  inplace_fill = on && FSEM_INPLACE_FLOATS;
+  return PyBool_FromLong(prev);
+}
+
 static PyMethodDef methods[] = {
+    {"set_inplace", set_inplace, METH_O,
+     "set_inplace(flag) -> previous: fill fresh floats in place (GIL builds <= 3.13 only) or by PyDict_SetItem"},
     {"score_list", score_list, METH_VARARGS, "score_list(scores_f32_KxB, keys) -> list of dicts"},
     {"score_list_alloc", score_list_alloc, METH_VARARGS,
      "score_list_alloc(B, keys) -> (list of B dicts with nan values, handle)"},
@@ -238,4 +267,8 @@ static PyMethodDef methods[] = {
 static struct PyModuleDef module = {PyModuleDef_HEAD_INIT, "_score_list", NULL, -1, methods,
                                     NULL, NULL, NULL, NULL};
 
-PyMODINIT_FUNC PyInit__score_list(void) { return PyModule_Create(&module); }
+PyMODINIT_FUNC PyInit__score_list(void) {
+  PyObject *m = PyModule_Create(&module);
+  if (m && PyModule_AddIntConstant(m, "INPLACE_COMPILED", FSEM_INPLACE_FLOATS) != 0) Py_CLEAR(m);
+  return m;
+}

@@ -993,6 +993,12 @@ extern "C" int fsem_version(void) { return 7; }  // 7: + fsem_host_buffer_mapped
 #endif
 static const char kBuildIdMarker[] = "FSEM_BUILD_ID:" FSEM_BUILD_ID;
 extern "C" const char *fsem_build_id(void) { return kBuildIdMarker + 14; }
+// The offload target, recorded apart from the content hash (_build.library_build_arch): a library
+// built for another target is refused at load rather than rebuilt.
+#ifndef FSEM_BUILD_ARCH
+#define FSEM_BUILD_ARCH "unknown"
+#endif
+__attribute__((used)) static const char kBuildArchMarker[] = "FSEM_BUILD_ARCH:" FSEM_BUILD_ARCH;
 
 // The drop-in call's scores go straight into its pinned host buffer when the runtime maps that
 // buffer into the device address space at the same address (hipHostMalloc memory on ROCm).

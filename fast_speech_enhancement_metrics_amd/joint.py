@@ -141,7 +141,7 @@ class PESQ_STOI(BaseMetric):
             wsb = self._ws_bytes[(B, L)] = lib.fsem_pesq_stoi_workspace_bytes(B, L)
         # the scores go straight into the thread's pinned host buffer when the device maps it
         # (no device->host copy behind the kernels: ~20 us of the step's idle tail)
-        slot = _native.mapped_host_slot(self, 3 * B) if self.host_scores and not device_scores else None
+        slot = _native.mapped_host_slot(self, 3 * B, dev) if self.host_scores and not device_scores else None
         if slot is not None:
             o = slot[0].data_ptr()
             outs = (o, o + 4 * B, o + 8 * B)

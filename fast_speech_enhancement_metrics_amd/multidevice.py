@@ -106,6 +106,11 @@ def in_shard() -> bool:
 class FanOut:
     """Host threads + streams of one metric's device list (kept across calls)."""
 
+    # test switch: a shard whose rows already live on its device takes the copy branch anyway (a
+    # copy on its copy stream of the source device, ordered by the same events), so the branch of
+    # a multi-GPU call runs -- and is checked bitwise -- on a one-GPU box
+    force_copy = False
+
     def __init__(self, devices: list[torch.device]):
         self.devices = devices
         self._pool = ThreadPoolExecutor(max_workers=len(devices), thread_name_prefix="fsem-shard")
@@ -180,7 +185,7 @@ class FanOut:
                 if in_ev is not None:
                     st.wait_event(in_ev)
                 c, n = clean[lo:hi], noisy[lo:hi]
-                if c.device == dev:
+                if c.device == dev and not self.force_copy:
                     # views of the caller's rows, read on this stream
                     c.record_stream(st)
                     n.record_stream(st)
@@ -188,9 +193,21 @@ class FanOut:
                 elif c.is_cuda:  # peer copy over xGMI on this shard's stream of the source device
                     cs = self._copy_stream(k, c.device)
                     cs.wait_event(in_ev)
+                    c.record_stream(cs)
+                    n.record_stream(cs)
                     with torch.cuda.stream(cs):
-                        c = c.to(dev, non_blocking=True)
-                        n = n.to(dev, non_blocking=True)
+                        if c.device == dev:  # force_copy: the same branch on one device
+                            c, n = c.clone(), n.clone()
+                        else:
+                            c = c.to(dev, non_blocking=True)
+                            n = n.to(dev, non_blocking=True)
+                        copied = torch.cuda.Event()
+                        copied.record(cs)
+                    # the shard's stream reads the copies after they land (explicit, beside PyTorch's
+                    # own barrier for cross-device copies) and owns them from here on
+                    st.wait_event(copied)
+                    c.record_stream(st)
+                    n.record_stream(st)
                     rec["input"] = cs.cuda_stream
                 else:  # host -> device on the shard's stream
                     c = c.to(dev, non_blocking=True)

@@ -72,3 +72,31 @@ def test_stale_library_is_refused_without_compiler(tree_copy, monkeypatch):
     monkeypatch.setattr(_build, "build", no_build)
     with pytest.raises(ImportError, match="stale"):
         _native._check_build_id()
+
+
+def test_stale_library_is_refused_without_opt_in(tree_copy, monkeypatch):
+    """A stale library is not rebuilt at import unless FSEM_AUTOBUILD=1 (every rank of a
+    multi-process job would otherwise run hipcc)."""
+    vad = tree_copy / "fsem_vad.h"
+    vad.write_text(vad.read_text() + "\n// edited\n")
+    calls = []
+    monkeypatch.setattr(_build, "build", lambda *a, **k: calls.append(1))
+    monkeypatch.delenv("FSEM_AUTOBUILD", raising=False)
+    with pytest.raises(ImportError, match="stale"):
+        _native._check_build_id()
+    assert not calls
+
+
+def test_other_target_is_refused_not_rebuilt(monkeypatch):
+    """A library built for another offload target is refused, never silently rebuilt for this one
+    (ADVICE r5); the target is recorded apart from the content hash, which it does not enter."""
+    assert _build.library_build_arch(_build.LIB) == _build.ARCH
+    h = _build.source_hash()
+    calls = []
+    monkeypatch.setattr(_build, "build", lambda *a, **k: calls.append(1))
+    monkeypatch.setattr(_build, "ARCH", "gfx942")
+    monkeypatch.setenv("FSEM_AUTOBUILD", "1")
+    assert _build.source_hash() == h
+    with pytest.raises(ImportError, match="built for gfx950"):
+        _native._check_build_id()
+    assert not calls

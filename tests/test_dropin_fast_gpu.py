@@ -114,7 +114,7 @@ def test_scores_written_into_mapped_host_buffer(pairs):
     m = PESQ_STOI(16000, use_gpu=True)
     assert _native.mapped_host_slot(m, 3 * B) is not None
     res = m(c, n)
-    host = m.__dict__["_fsem_tls"].np[:3 * B].reshape(3, B)
+    host = m.__dict__["_fsem_tls"].slots[c.device.index][1][:3 * B].reshape(3, B)
     np.testing.assert_array_equal(host[0], np.array([d["PESQ"] for d in res], np.float32))
     np.testing.assert_array_equal(host[2], np.array([d["ESTOI"] for d in res], np.float32))
     cp = PESQ_STOI(16000, use_gpu=True)

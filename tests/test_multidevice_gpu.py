@@ -165,3 +165,89 @@ def test_time_alignment_delays_keep_int32_through_fanout(pairs):
     mos, d = fo.run(score, c, c, None, 2)
     assert d.dtype == torch.int32 and mos.dtype == torch.float32
     np.testing.assert_array_equal(d.cpu().numpy(), big.cpu().numpy())
+
+
+def test_forced_copy_branch_on_one_gpu(pairs):
+    """The peer-copy branch of a shard whose rows live on another device, run on
+    the 1-GPU box by FanOut.force_copy: each shard's rows are copied on its own copy stream of the
+    source device, after the event of the caller's stream, and its compute stream waits for the
+    copy's event -- scores bitwise those of the single-device call, also from a non-default caller
+    stream, and the recorded input streams are the per-shard copy streams, not the compute
+    streams."""
+    from fast_speech_enhancement_metrics_amd import PESQ_STOI
+    c, n = pairs
+    want = _np(PESQ_STOI(16000, use_gpu=True).scores(c, n))
+    m = PESQ_STOI(16000, use_gpu=True, devices=[0, 0, 0])
+    m._fanout.force_copy = True
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        s.wait_stream(torch.cuda.default_stream())
+        # inputs produced on the caller's stream right before the call: the copies must wait for them
+        c2, n2 = c * 1.0, n * 1.0
+        got = m.scores(c2, n2)
+        res = m(c2, n2)
+        got = [t.clone() for t in got]
+    s.synchronize()
+    for a, b in zip(_np(got), want):
+        np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(np.array([d["PESQ"] for d in res], np.float32), want[0])
+    np.testing.assert_array_equal(np.array([d["ESTOI"] for d in res], np.float32), want[2])
+    rec = m._fanout.last_copy_streams
+    assert len(rec) == 3 and all(r is not None for r in rec)
+    assert all(r["input"] != r["compute"] for r in rec)
+    assert len({r["input"] for r in rec}) == 3
+    assert s.cuda_stream not in {r["input"] for r in rec}
+    dev0 = torch.device("cuda", 0)
+    assert {r["input"] for r in rec} == {m._fanout._copy_stream(k, dev0).cuda_stream for k in range(3)}
+
+
+def test_host_slots_keyed_by_device(pairs):
+    """The drop-in call's pinned score buffer and event are kept per (thread, device)."""
+    from fast_speech_enhancement_metrics_amd import PESQ_STOI
+    c, n = pairs
+    m = PESQ_STOI(16000, use_gpu=True)
+    m(c, n)
+    assert set(m.__dict__["_fsem_tls"].slots) == {0}
+    m.release()
+    assert "_held_list" not in m.__dict__ and not m.__dict__["_fsem_tls"].slots
+    assert [d["PESQ"] for d in m(c, n)] == [d["PESQ"] for d in PESQ_STOI(16000, use_gpu=True)(c, n)]
+
+
+needs_two = pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two HIP devices")
+
+
+@needs_two
+def test_two_devices_peer_copies(pairs):
+    """devices=[0, 1] with the batch on cuda:0: shard 1 pulls its rows over xGMI on its copy stream of
+    cuda:0 and its scores come back to cuda:0; bitwise the single-device scores, from a non-default
+    caller stream."""
+    from fast_speech_enhancement_metrics_amd import PESQ_STOI
+    c, n = pairs
+    want = _np(PESQ_STOI(16000, use_gpu=True).scores(c, n))
+    m = PESQ_STOI(16000, use_gpu=True, devices=[0, 1])
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        s.wait_stream(torch.cuda.default_stream())
+        got = [t.clone() for t in m.scores(c, n)]
+    s.synchronize()
+    assert all(t.device == torch.device("cuda", 0) for t in got)
+    for a, b in zip(_np(got), want):
+        np.testing.assert_array_equal(a, b)
+    rec = m._fanout.last_copy_streams
+    assert rec[0]["input"] == rec[0]["compute"]
+    assert rec[1]["input"] == m._fanout._copy_stream(1, torch.device("cuda", 0)).cuda_stream != rec[1]["compute"]
+
+
+@needs_two
+def test_metric_called_on_two_devices(pairs):
+    """One metric object called on cuda:0 and then with cuda:1 current: its per-thread
+    host slot and event are per device, so the second call neither fails nor mixes devices."""
+    from fast_speech_enhancement_metrics_amd import PESQ_STOI
+    c, n = pairs
+    m = PESQ_STOI(16000, use_gpu=True)
+    want = m(c, n)
+    with torch.cuda.device(1):
+        got = m(c.to("cuda:1"), n.to("cuda:1"))
+    assert [d["PESQ"] for d in got] == [d["PESQ"] for d in want]
+    assert [d["STOI"] for d in got] == [d["STOI"] for d in want]
+    assert set(m.__dict__["_fsem_tls"].slots) == {0, 1}

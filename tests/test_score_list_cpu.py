@@ -184,3 +184,39 @@ def test_fill_rejects_mismatched_keys_of_equal_count(builder):
     assert all(math.isnan(v) for d in lst for v in d.values())  # nothing written by the refused calls
     _native.score_list_fill(h, 0, scores, tuple(["STOI", "E" + "STOI"]))
     assert lst == [{"STOI": 0.5, "ESTOI": 1.0}, {"STOI": 0.25, "ESTOI": 2.0}]
+
+
+def test_fill_dict_path_equals_inplace_path():
+    """score_list_fill writes fresh floats in place only on GIL builds of CPython <= 3.13 (VERDICT
+    r5 item 5: it relies on their refcount semantics); elsewhere, and with set_inplace(False),
+    every value goes through PyDict_SetItem.  Both forms give the same list, also for rows the
+    caller touched in between."""
+    import sys
+    import sysconfig
+    mod = _native._load_score_list()
+    assert mod is not False
+    free_threaded = bool(sysconfig.get_config_var("Py_GIL_DISABLED"))
+    assert mod.INPLACE_COMPILED == int(not free_threaded and sys.version_info < (3, 14))
+    g = torch.Generator().manual_seed(5)
+    t = torch.randn(3, 257, generator=g).numpy()
+    t[2, 9] = float("nan")
+    keys = ("PESQ", "STOI", "ESTOI")
+    lists = []
+    for inplace in (True, False):
+        prev = mod.set_inplace(inplace)
+        try:
+            lst, h = _native.score_list_alloc(257, keys)
+            held = lst[4]["STOI"]  # a value the caller holds: filled by a new float either way
+            _native.score_list_fill(h, 0, t[:, :100].copy(), keys)
+            _native.score_list_fill(h, 100, t[:, 100:].copy(), keys)
+            assert math.isnan(held)
+            lists.append(lst)
+        finally:
+            mod.set_inplace(prev)
+    ref = _py(torch.from_numpy(t), keys)
+    for lst in lists:
+        assert len(lst) == 257
+        for a, b in zip(lst, ref):
+            for k in keys:
+                assert (math.isnan(a[k]) and math.isnan(b[k])) or a[k] == b[k]
+    assert mod.set_inplace(True) == bool(mod.INPLACE_COMPILED)
