@@ -63,6 +63,13 @@ __device__ unsigned long long g_stamps[kStampBlocks][16];
   } while (0)
 #endif
 
+// Diagnostic builds only (tools/ab_front.py): FSEM_DOUBLE = k runs phase k
+// of pesq_front twice per item (1 resampler, 2 IIR pass 1, 3 chunk scan, 4 FFTs, 5 IIR pass 2)
+// -- the marginal wall time of a phase inside the full kernel; the outputs are not meaningful.
+#ifndef FSEM_DOUBLE
+#define FSEM_DOUBLE 0
+#endif
+
 constexpr int PT = 256;
 constexpr int CH = FSEM_PESQ_CH;  // 52 samples per lane (stride 208 B: conflict-free b128)
 constexpr int TILE = PT * CH;     // 13312
@@ -725,6 +732,9 @@ __global__ void __launch_bounds__(PT, 2)
       float2 *vrow = (vad && it.s < B) ? vad + b * v_ld : nullptr;  // clean rows only
       resample_tile(tile, o_lo, o_hi, y10 + (2 * b + (it.s < B ? 0 : 1)) * y_ld, vrow, vwa, vwb, rsb,
                     xbuf + RS_STAGE * wave, lane, wave);
+      if (FSEM_DOUBLE == 1)
+        resample_tile(tile, o_lo, o_hi, y10 + (2 * b + (it.s < B ? 0 : 1)) * y_ld, vrow, vwa, vwb, rsb,
+                      xbuf + RS_STAGE * wave, lane, wave);
     }
     STAMP(1);
     const int g = it.g;
@@ -760,6 +770,17 @@ __global__ void __launch_bounds__(PT, 2)
       iir_pass1<true>(my4, t_lane, L, xm1, xm1 - xm2, xr1, e);
     else
       iir_pass1<false>(my4, t_lane, L, xm1, xm1 - xm2, xm1, e);
+    if (FSEM_DOUBLE == 2) {
+      const float4 *m2 = my4;
+      asm volatile("" : "+v"(m2));
+      float e2[NS];
+      if (__builtin_amdgcn_readfirstlane((int)wave_edge))
+        iir_pass1<true>(m2, t_lane, L, xm1, xm1 - xm2, xr1, e2);
+      else
+        iir_pass1<false>(m2, t_lane, L, xm1, xm1 - xm2, xm1, e2);
+#pragma unroll
+      for (int i = 0; i < NS; ++i) e[i] = (e[i] + e2[i]) * 0.5f;
+    }
     // The tile's scale for its range shift (below): the peak magnitude of the chunks' end
     // states, which bound both filters' outputs -- the quantities squared from pass 2 on -- to
     // within the filters' gains (a factor ~100, far inside the shift's [2^-40, 2^40] window);
@@ -801,7 +822,8 @@ __global__ void __launch_bounds__(PT, 2)
     put_states(scan_at(false, tid));
     lds_barrier();
 #pragma unroll
-    for (int lv = 0; lv < 4; ++lv) {
+    for (int lv8 = 0; lv8 < (FSEM_DOUBLE == 3 ? 8 : 4); ++lv8) {
+      const int lv = lv8 & 3;
       const int d = 1 << lv;
       float q[NS];
       // lanes without a chunk d back read the zero row (an address select instead of 12
@@ -874,6 +896,14 @@ __global__ void __launch_bounds__(PT, 2)
         acc = iir_pass2_split(w4, z, own_lo, own_hi, xm1, xm1 - xm2);
       else
         acc = iir_pass2_masked<false>(w4, z, own_lo, own_hi, lim, t_lane, L, xm1, xm1 - xm2);
+      if (FSEM_DOUBLE == 5) {  // again over the (rewritten) chunk, from the same start state
+        float z2[NS];
+#pragma unroll
+        for (int i = 0; i < NS; ++i) z2[i] = z[i] * 0.5f;
+        acc += __builtin_amdgcn_readfirstlane((int)__all(split_ok)) && !__builtin_amdgcn_readfirstlane((int)wave_edge)
+                   ? iir_pass2_split(w4, z2, own_lo, own_hi, xm1, xm1 - xm2)
+                   : iir_pass2_masked<false>(w4, z2, own_lo, own_hi, lim, t_lane, L, xm1, xm1 - xm2);
+      }
       // per-wave partials (no workgroup barrier); pesq_power_sum adds them in a fixed order
       const float tot = wave_sum_dpp(acc);
       if (lane == 0) ppart[(it.s * nseg + g) * 4 + wave] = tot * (kBpGain * kBpGain);
@@ -920,6 +950,7 @@ __global__ void __launch_bounds__(PT, 2)
             v[r] = {w2.x, w2.y};
           }
           fft512_wave(v, wbuf, lane, tw1, tw2);
+          if (FSEM_DOUBLE == 4) fft512_wave(v, wbuf, lane, tw1, tw2);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             float mr = __shfl(v[7 - r].r, plane, 64);

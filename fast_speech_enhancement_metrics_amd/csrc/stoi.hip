@@ -334,6 +334,20 @@ __device__ __forceinline__ uint32_t peak_exponents(float c0, float c1, float c2,
   return __builtin_amdgcn_readlane(e, 63);
 }
 
+// Powers of one transform in the wave's exchange area, bin k of frame a at tob_pw(k), of frame b
+// at TOB_PB + tob_pw(k): bins from 128 on 3 words further, which makes the band sums' 12 piece
+// reads (lane l reads its piece start + i) 2-way instead of 3-way bank conflicts in each 32-lane
+// half (the piece starts of kObmPiece, gen_tables.py, never straddle bin 128; round 6, 24 fewer
+// LDS cycles per transform of ~230); the stores stay lane-linear (64-bin rows, one offset each).
+constexpr int TOB_PB = 264;
+__device__ __forceinline__ constexpr int tob_pw(int k) { return k + (k >= 128 ? 3 : 0); }
+constexpr bool tob_pieces_unsplit() {
+  for (int l = 0; l < 64; ++l)
+    if (kObmPiece[l][2] < 128 && kObmPiece[l][3] > 128) return false;
+  return true;
+}
+static_assert(tob_pieces_unsplit() && 2 * TOB_PB <= 2 * kFftBuf - 12, "padded band-sum layout");
+
 constexpr int TOB_WAVES = 4;  // 256-thread workgroups (8 waves x 66 KB measured no faster)
 __global__ void __launch_bounds__(64 * TOB_WAVES)
     stoi_tob(const float *__restrict__ y10, int64_t y_ld, int64_t B, Rows rows, const int *__restrict__ idx,
@@ -413,6 +427,8 @@ __global__ void __launch_bounds__(64 * TOB_WAVES)
   const int plane = (64 - lane) & 63;
   const int pc_sig = kObmPiece[lane][0], pc_band = kObmPiece[lane][1];
   const int pc_lo = kObmPiece[lane][2], pc_hi = kObmPiece[lane][3];
+  // this lane's piece in the padded power layout (tob_pw): no piece crosses bin 128
+  const int pc_at = TOB_PB * pc_sig + tob_pw(pc_lo);
   const int pc_gs = kObmPiece[lane][4];
   const bool pc_head = kObmPiece[lane][5] != 0;
   // Two consecutive STFT frames of ONE signal per complex FFT (z = frame a + i frame b): the
@@ -489,18 +505,18 @@ __global__ void __launch_bounds__(64 * TOB_WAVES)
     // per transform: the kernel is issue bound, SQ_INSTS_SALU 45 % of its VALU count)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      pbuf[64 * r + lane] = pa[r];
-      pbuf[256 + 64 * r + lane] = pb[r];
+      pbuf[tob_pw(64 * r) + lane] = pa[r];
+      pbuf[TOB_PB + tob_pw(64 * r) + lane] = pb[r];
     }
     wave_lds_fence();
     {
-      // band sums: one <=9-bin piece per lane (lanes of piece set 0: frame a, set 1: frame b),
+      // band sums: one <=12-bin piece per lane (lanes of piece set 0: frame a, set 1: frame b),
       // segmented shuffle reduction per band
-      const float *ps = pbuf + 256 * pc_sig;
-      float acc = (pc_lo < pc_hi) ? ps[pc_lo] : 0.f;
+      const float *ps = pbuf + pc_at;
+      float acc = (pc_lo < pc_hi) ? ps[0] : 0.f;
 #pragma unroll
-      for (int i = 1; i < 12; ++i) {  // unconditional reads (inside the frame's 256 powers), masked adds
-        const float x = ps[pc_lo + i];
+      for (int i = 1; i < 12; ++i) {  // unconditional reads (inside the frame's powers), masked adds
+        const float x = ps[i];
         acc += (pc_lo + i < pc_hi) ? x : 0.f;
       }
       // each band's group (1, 2 or 4 lanes, aligned inside a 16-lane row): two in-row DPP steps

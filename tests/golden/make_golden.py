@@ -283,7 +283,7 @@ def edge_case(name: str = "edges_16k"):
 
 
 def tone_probe_case(name: str = "tone_probe_10k"):
-    """tools/tone_probe.py's inputs at 10 kHz: full-scale float32 sinusoids (250 / 1000 / 3150 Hz)
+    """tools/probes/tone_probe.py's inputs at 10 kHz: full-scale float32 sinusoids (250 / 1000 / 3150 Hz)
     against the tone + 1e-3 noise, and tone + 0.05 noise against the pure tone -- scores near 0
     and 1 where the segment statistics correlate rounding-level fluctuations.  Stored as float32
     rows (clean_f32 / noisy_f32); STOI(10000) with torch seeds 0 and 1."""

@@ -100,7 +100,7 @@ def test_stoi_huge_scale(edges):
 
 @pytest.mark.parametrize("golden", ["tone_probe_10k", "lowpass_10k"])
 def test_10k_probes_match_reference(golden):
-    """tone_probe_10k: full-scale tones against tone + noise (tools/tone_probe.py) -- scores near 0
+    """tone_probe_10k: full-scale tones against tone + noise (tools/probes/tone_probe.py) -- scores near 0
     correlate rounding-level fluctuations of nearly constant envelopes, and the reference's own
     float32 result moves by up to ~1e-2 under a re-scaling of the same input.  lowpass_10k: a
     low-passed denoised signal (upper bands 80-100 dB below the clean's, peaks within a factor
