@@ -37,12 +37,13 @@ class PESQ(BaseMetric):
         """``time_align`` (extension, off by default as in the reference, PESQ.py:19-22): shift each
         degraded row by its estimated delay before scoring (``alignment.time_align``, P.862-style;
         ``max_delay`` samples at 16 kHz bounds the search): True or "row" -- one delay per row;
-        "utterance" -- P.862's per-utterance delays, the row realigned segment by segment.  The
-        delays of the last scored batch (per row; in utterance mode each row's longest segment's)
-        are kept in ``last_delays``.  ``devices``: see BaseMetric (multi-device calls)."""
+        "utterance" -- P.862's per-utterance delays, the row realigned segment by segment;
+        "p862" -- the same with P.862's histogram fine stage and recursive utterance split.  The
+        delays of the last scored batch (per row; in the segment modes each row's longest
+        segment's) are kept in ``last_delays``.  ``devices``: see BaseMetric (multi-device calls)."""
         super().__init__(sample_rate, use_gpu, devices=devices)
-        if time_align not in (False, True, "row", "utterance"):
-            raise ValueError('time_align must be False, True, "row" or "utterance"')
+        if time_align not in (False, True, "row", "utterance", "p862"):
+            raise ValueError('time_align must be False, True, "row", "utterance" or "p862"')
         self.time_align = "row" if time_align is True else time_align
         self.max_delay = int(max_delay)
         self.last_delays = None

@@ -418,8 +418,47 @@ def _ta_piece_xcorr(wr, wd, a: int, b: int, lo: int, hi: int) -> np.ndarray:
     return _xcorr_window(wr[a:b], win, 0, hi - lo) if b > a else np.zeros(hi - lo + 1)
 
 
-def time_align_utt_row(ref: np.ndarray, deg: np.ndarray, max_delay: int):
-    """(seg_start [n+1], seg_delay [n], row delay) of one row (csrc/align.hip, utterance mode)."""
+# P.862 mode (csrc/align.hip stages 10-12; P.862 sections 10.5-10.6 on the fine stage's pieces)
+_TA_HIST_T, _TA_HIST_POW, _TA_REL_MIN, _TA_MAXDEPTH, _TA_MAXSEG = 8, 0.125, 0.05, 2, 32
+
+
+def _ta_hist(pv: np.ndarray, pl: np.ndarray, a: int, b: int, d0: int):
+    """(delay, confidence, voting pieces) of pieces [a, b): the first maximum of the triangle-
+    smoothed histogram of the voting pieces' peak lags, weighted by peak^0.125."""
+    sel = np.flatnonzero(pl[a:b] >= 0) + a
+    if sel.size == 0:
+        return d0, 0.0, 0
+    H = np.zeros(2 * _TA_FINE + 1)
+    for i in sel:  # piece order, as the engine adds them
+        H[pl[i]] += pv[i] ** _TA_HIST_POW
+    k = np.arange(-_TA_HIST_T, _TA_HIST_T + 1)
+    S = np.convolve(H, (_TA_HIST_T + 1 - np.abs(k)).astype(np.float64), mode="same")
+    j = int(np.argmax(S))
+    return d0 - _TA_FINE + j, float(S[j] / ((_TA_HIST_T + 1) * H.sum())), int(sel.size)
+
+
+def _ta_split_p862(pv, pl, a: int, b: int, d0: int, depth: int) -> list:
+    """[(piece offset from a, delay)]: pieces [a, b) split where both halves (two or more voting
+    pieces each) disagree by SPLIT_MIN and are more confident than the whole, recursively."""
+    D, c, _ = _ta_hist(pv, pl, a, b, d0)
+    if depth < _TA_MAXDEPTH and b - a >= 4:
+        best = None
+        for sp in range(a + 2, b - 1):
+            dL, cL, nL = _ta_hist(pv, pl, a, sp, d0)
+            dR, cR, nR = _ta_hist(pv, pl, sp, b, d0)
+            ok = nL >= 2 and nR >= 2 and abs(dL - dR) >= _TA_SPLIT_MIN and cL > c and cR > c
+            if ok and (best is None or cL + cR > best[0]):
+                best = (cL + cR, sp)
+        if best is not None:
+            sp = best[1]
+            right = _ta_split_p862(pv, pl, sp, b, d0, depth + 1)
+            return _ta_split_p862(pv, pl, a, sp, d0, depth + 1) + [(sp - a + o, d) for o, d in right]
+    return [(0, D)]
+
+
+def time_align_utt_row(ref: np.ndarray, deg: np.ndarray, max_delay: int, mode: str = "utterance"):
+    """(seg_start [n+1], seg_delay [n], row delay) of one row (csrc/align.hip, utterance or P.862
+    mode)."""
     r = np.asarray(ref, dtype=np.float64)
     d = np.asarray(deg, dtype=np.float64)
     L = r.shape[0]
@@ -451,6 +490,15 @@ def time_align_utt_row(ref: np.ndarray, deg: np.ndarray, max_delay: int):
         m = max(1, -(-(R[u + 1] - R[u]) // _TA_CHUNK))
         P = np.stack([_ta_piece_xcorr(wr, wd, R[u] + i * _TA_CHUNK, min(R[u] + (i + 1) * _TA_CHUNK, R[u + 1]),
                                       d0 - _TA_FINE, d0 + _TA_FINE) for i in range(m)])
+        if mode == "p862":
+            pl = np.array([_first_max(P[i]) for i in range(m)])
+            pv = np.array([P[i, j] if j >= 0 else 0.0 for i, j in enumerate(pl)])
+            pl[pv < _TA_REL_MIN * pv.max()] = -1
+            for off, D in _ta_split_p862(pv, pl, 0, m, d0, 0):
+                if not (delays and delays[-1] == D) and len(delays) < _TA_MAXSEG:
+                    starts.append(R[u] + off * _TA_CHUNK)
+                    delays.append(D)
+            continue
         W = P.sum(axis=0)
         iW = _first_max(W)
         segs = [(0, d0 - _TA_FINE + iW if iW >= 0 else d0)]
@@ -475,7 +523,8 @@ def time_align_utt_row(ref: np.ndarray, deg: np.ndarray, max_delay: int):
     return np.array(starts), np.array(delays), int(delays[int(np.argmax(lens))])
 
 
-def time_align_utterances(clean: torch.Tensor, noisy: torch.Tensor, lengths=None, max_delay: int = 16000):
+def time_align_utterances(clean: torch.Tensor, noisy: torch.Tensor, lengths=None, max_delay: int = 16000,
+                          mode: str = "utterance"):
     """(aligned [B, L] f32, delays [B], n_seg [B], seg_start [B, 33], seg_delay [B, 32]) int32."""
     c = clean.detach().cpu().numpy()
     n = noisy.detach().cpu().numpy()
@@ -487,7 +536,7 @@ def time_align_utterances(clean: torch.Tensor, noisy: torch.Tensor, lengths=None
     st = np.zeros((B, S + 1), dtype=np.int32)
     sd = np.zeros((B, S), dtype=np.int32)
     rows = [L if lengths is None else int(min(max(int(lengths[b]), 0), L)) for b in range(B)]
-    res = _host_map(lambda b: time_align_utt_row(c[b, :rows[b]], n[b, :rows[b]], max_delay), range(B))
+    res = _host_map(lambda b: time_align_utt_row(c[b, :rows[b]], n[b, :rows[b]], max_delay, mode), range(B))
     for b, (starts, delays, D) in enumerate(res):
         k = len(delays)
         ns[b], ds[b] = k, D

@@ -62,6 +62,9 @@ SIGNATURES = {
     "fsem_time_align_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _c_i32, _vp, _vp, _c_i64, _vp,
                                             _c_sz, _vp]),
     "fsem_time_align_utt_workspace_bytes": (_c_sz, [_c_i64, _c_i64]),
+    "fsem_time_align_p862_workspace_bytes": (_c_sz, [_c_i64, _c_i64]),
+    "fsem_time_align_p862_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _c_i32, _vp, _vp, _vp, _vp,
+                                                 _vp, _c_i64, _vp, _c_sz, _vp]),
     "fsem_time_align_utt_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _c_i32, _vp, _vp, _vp, _vp,
                                                 _vp, _c_i64, _vp, _c_sz, _vp]),
 }

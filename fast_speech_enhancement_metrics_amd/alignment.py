@@ -21,7 +21,15 @@ delay) and fine delay (as above, over its region), and a region splits once wher
 change within it raises the summed correlation peak by 20 %.  The degraded row is realigned
 segment by segment; ``delays`` is then each row's longest segment's delay.
 
-GPU rows run ``fsem_time_align_f32`` / ``fsem_time_align_utt_f32`` (``csrc/align.hip``); CPU rows
+``mode="p862"`` completes P.862's per-utterance stages (sections 10.5-10.6) on the same pieces:
+each 320 ms piece of an utterance's region votes for its correlation peak's lag (weight
+peak^0.125, pieces under 5 % of the utterance's largest peak do not vote), a range of pieces takes
+the first maximum of its triangle-smoothed vote histogram as delay and that maximum's share of
+the votes as confidence, and a range splits where both halves are more confident and disagree by
+1 ms or more -- recursively, two levels (up to 4 segments per utterance).
+
+GPU rows run ``fsem_time_align_f32`` / ``fsem_time_align_utt_f32`` / ``fsem_time_align_p862_f32``
+(``csrc/align.hip``); CPU rows
 the float64 FFT form in ``_cpu.py``.  Parity against P.862 implementations is unpinned (none is importable here); the
 tests pin both paths to ``oracle/align_oracle.py`` and to known synthetic delays.
 """
@@ -35,7 +43,7 @@ from .base import as_rows, device_lengths
 DEFAULT_MAX_DELAY = 16000  # samples at 16 kHz (1 s)
 
 
-MODES = ("row", "utterance")
+MODES = ("row", "utterance", "p862")
 
 
 def _prepare(clean, noisy, max_delay):
@@ -67,13 +75,13 @@ def time_align(clean: torch.Tensor, noisy: torch.Tensor, lengths=None,
 
     ``lengths`` (optional [B] ints): row b holds lengths[b] samples; the aligned row is zero
     past them.  ``max_delay``: the crude search range in samples (rounded up to 4 ms frames).
-    ``mode``: "row" (one delay per row) or "utterance" (per-utterance delays, see
+    ``mode``: "row" (one delay per row), "utterance" or "p862" (per-utterance delays, see
     ``time_align_segments``; ``delays`` = each row's longest segment's delay).
     """
     if mode not in MODES:
         raise ValueError(f"mode must be one of {MODES}")
-    if mode == "utterance":
-        out, delays, *_ = time_align_segments(clean, noisy, lengths, max_delay)
+    if mode in ("utterance", "p862"):
+        out, delays, *_ = time_align_segments(clean, noisy, lengths, max_delay, mode=mode)
         return out, delays
     c, n, max_delay = _prepare(clean, noisy, max_delay)
     B, L = c.shape
@@ -94,19 +102,22 @@ def time_align(clean: torch.Tensor, noisy: torch.Tensor, lengths=None,
 
 
 def time_align_segments(clean: torch.Tensor, noisy: torch.Tensor, lengths=None,
-                        max_delay: int = DEFAULT_MAX_DELAY):
-    """Per-utterance alignment (P.862 sections 10.3-10.5, see the module docstring) of 16 kHz rows.
+                        max_delay: int = DEFAULT_MAX_DELAY, mode: str = "utterance"):
+    """Per-utterance alignment (P.862 sections 10.3-10.5, or with ``mode="p862"`` 10.3-10.6, see the
+    module docstring) of 16 kHz rows.
 
     Returns (aligned [B, L] float32, delays [B], n_seg [B], seg_start [B, 33], seg_delay [B, 32])
     on the rows' device (int32 but ``aligned``): segment k of row b covers samples
     [seg_start[b, k], seg_start[b, k + 1]) for k < n_seg[b] and is shifted by seg_delay[b, k];
     ``delays`` is each row's longest segment's delay.
     """
+    if mode not in ("utterance", "p862"):
+        raise ValueError('mode must be "utterance" or "p862"')
     c, n, max_delay = _prepare(clean, noisy, max_delay)
     B, L = c.shape
     if not c.is_cuda:
         lens = None if lengths is None else device_lengths(lengths, B, L, "cpu")
-        return _cpu.time_align_utterances(c, n, lens, max_delay)
+        return _cpu.time_align_utterances(c, n, lens, max_delay, mode=mode)
     lib = _native.load()
     lens = device_lengths(lengths, B, L, c.device) if lengths is not None else None
     c, n = _device_rows(c, n)
@@ -115,10 +126,11 @@ def time_align_segments(clean: torch.Tensor, noisy: torch.Tensor, lengths=None,
     i32 = dict(dtype=torch.int32, device=c.device)
     delays, nseg = torch.empty(B, **i32), torch.empty(B, **i32)
     starts, sdel = torch.zeros(B, S + 1, **i32), torch.zeros(B, S, **i32)
-    ws = _native.workspace(lib.fsem_time_align_utt_workspace_bytes(B, L), c.device)
-    _native.check(lib.fsem_time_align_utt_f32(c.data_ptr(), n.data_ptr(), B, L, c.stride(0),
-                                              lens.data_ptr() if lens is not None else None, max_delay,
-                                              delays.data_ptr(), nseg.data_ptr(), starts.data_ptr(),
-                                              sdel.data_ptr(), out.data_ptr(), out.stride(0), ws.data_ptr(),
-                                              ws.numel(), _native.stream_handle(c.device)), "time alignment")
+    wsb, entry = ((lib.fsem_time_align_p862_workspace_bytes, lib.fsem_time_align_p862_f32) if mode == "p862"
+                  else (lib.fsem_time_align_utt_workspace_bytes, lib.fsem_time_align_utt_f32))
+    ws = _native.workspace(wsb(B, L), c.device)
+    _native.check(entry(c.data_ptr(), n.data_ptr(), B, L, c.stride(0), lens.data_ptr() if lens is not None else None,
+                        max_delay, delays.data_ptr(), nseg.data_ptr(), starts.data_ptr(), sdel.data_ptr(),
+                        out.data_ptr(), out.stride(0), ws.data_ptr(), ws.numel(), _native.stream_handle(c.device)),
+                  "time alignment")
     return out, delays, nseg, starts, sdel

@@ -24,6 +24,16 @@
 //      ta_segments: the row's segments (equal neighbours merged) and its longest segment's delay;
 //   9. ta_shift_seg: a[n] = deg[n + D_k] in segment k.
 //
+// P.862 mode (fsem_time_align_p862_f32, oracle/align_oracle.py steps 10-12; P.862 sections
+// 10.5-10.6 restated on stage 7's 320 ms pieces): stages 5-7 as the utterance mode, then
+//  10. ta_piece_peaks (a wave per piece): the piece's correlation peak and its lag;
+//  11-12. ta_pick_p862 (workgroup per utterance): the pieces from 5 % of the utterance's largest
+//      peak vote for their lags with weight peak^0.125 (P.862's histogram), the triangle-smoothed
+//      histogram's first maximum is a range's delay and its share of the votes its confidence; a
+//      range splits at the piece boundary whose two halves (two or more votes each, delays >= 1 ms
+//      apart) are both more confident than the whole, the most confident pair first, and each
+//      half once more (P.862 utterance_split, two levels: up to 4 segments per utterance);
+//      ta_segments_p862: the row's segments as in stage 8, at most MAXSEG.
 // Cost is set by stage 3: 767 lags x L multiply-adds per row (about 123 M for 10 s), as
 // register-blocked packed FMAs out of LDS (16 consecutive lags per lane sliding over the chunk);
 // the other stages are O(L) or O(M * L / 64).
@@ -651,6 +661,197 @@ __global__ void __launch_bounds__(256) ta_shift_seg(const float *__restrict__ de
   }
 }
 
+// ---------------------------------------------------------------- P.862 mode stages 10-12
+constexpr int HIST_T = 8;            // lags: half-width of the histogram's triangle
+constexpr double HIST_POW = 0.125;   // a piece's vote: its correlation peak to this power
+constexpr double REL_MIN = 0.05;     // votes from this fraction of the utterance's largest peak
+constexpr int USEG_P = 8;            // per utterance: {segments, 3 piece offsets, 4 delays}
+
+// One wave per piece slot: the first maximum above zero of its NLAG partials, (value, lag index),
+// or (0, -1).  Keys (value bits, ~lag) order positive floats as values, ties to the smaller lag.
+__global__ void __launch_bounds__(256) ta_piece_peaks(int64_t nslot_total, const float *__restrict__ part,
+                                                      float *__restrict__ pv, int *__restrict__ pl) {
+  const int64_t slot = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (slot >= nslot_total) return;  // wave-uniform
+  const int lane = threadIdx.x & 63;
+  const float *P = part + slot * (int64_t)(NGRP * LG);
+  unsigned long long key = 0;
+  for (int l = lane; l < NLAG; l += 64) {
+    const float v = P[l];
+    const unsigned long long k =
+        v > 0.f ? ((unsigned long long)__float_as_uint(v) << 32) | (unsigned)(0xFFFFFFFFu - (unsigned)l) : 0ull;
+    key = k > key ? k : key;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const unsigned long long k2 = __shfl_xor(key, off, 64);
+    key = k2 > key ? k2 : key;
+  }
+  if (lane == 0) {
+    pv[slot] = key ? __uint_as_float((unsigned)(key >> 32)) : 0.f;
+    pl[slot] = key ? (int)(0xFFFFFFFFu - (unsigned)key) : -1;
+  }
+}
+
+// Workgroup (utterance u, row b): its m pieces' peaks, the votes (REL_MIN of the largest), then
+// up to three range evaluations' split searches (stage 12).  A range's histogram is rebuilt from
+// its pieces for every evaluation, each lag's votes added in piece order (double).
+__global__ void __launch_bounds__(256) ta_pick_p862(int64_t B, const int *__restrict__ nutt, const int *__restrict__ cs,
+                                                    const int *__restrict__ ucrude, int nslot,
+                                                    const float *__restrict__ pv, const int *__restrict__ pl,
+                                                    int *__restrict__ useg) {
+  __shared__ double sv[4];
+  __shared__ int sj[4];
+  __shared__ double H[NGRP * LG + 2 * HIST_T];  // lag l at H[HIST_T + l]; zero margins
+  const int u = blockIdx.x;
+  const int64_t b = blockIdx.y + (int64_t)blockIdx.z * 65535;
+  if (b >= B || u >= nutt[b]) return;
+  const int tid = threadIdx.x;
+  const int c0 = cs[b * (MAXU + 1) + u], m = cs[b * (MAXU + 1) + u + 1] - c0;
+  const float *v = pv + b * nslot + c0;
+  const int *lg = pl + b * nslot + c0;
+  const int d0 = ucrude[b * MAXU + u];
+  // the utterance's largest piece peak
+  double vmax = 0.0;
+  for (int i = tid; i < m; i += 256) vmax = fmax(vmax, (double)v[i]);
+  {
+    int dummy = 0;
+    block_argmax(vmax, dummy, sv, sj);
+  }
+  const double vmin = REL_MIN * vmax;
+  auto votes = [&](int i) { return lg[i] >= 0 && (double)v[i] >= vmin; };
+  // (delay, confidence, votes) of pieces [a, e): every thread the same values
+  auto eval = [&](int a, int e, int &D, double &conf, int &nv) {
+    __syncthreads();  // the previous evaluation's readers of H are done
+    for (int l = tid; l < NGRP * LG + 2 * HIST_T; l += 256) H[l] = 0.0;
+    __syncthreads();
+    int cnt = 0;
+    double h[3] = {0.0, 0.0, 0.0};
+    for (int i = a; i < e; ++i) {  // piece order; the thread's own lags only
+      if (!votes(i)) continue;
+      ++cnt;
+      const int l = lg[i];
+      if ((l & 255) == tid) h[l >> 8] += pow((double)v[i], HIST_POW);
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      if (tid + 256 * q < NLAG) H[HIST_T + tid + 256 * q] = h[q];
+    __syncthreads();
+    double tot = 0.0;
+    for (int l = 0; l < NLAG; ++l) tot += H[HIST_T + l];  // lag order (every thread)
+    double best = -1.0;
+    int arg = INT32_MAX;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int l = tid + 256 * q;
+      if (l >= NLAG) continue;
+      double sm = 0.0;
+#pragma unroll
+      for (int k = -HIST_T; k <= HIST_T; ++k) sm += (double)(HIST_T + 1 - abs(k)) * H[HIST_T + l + k];
+      if (sm > best) {
+        best = sm;
+        arg = l;
+      }
+    }
+    block_argmax(best, arg, sv, sj);
+    nv = cnt;
+    if (cnt == 0) {
+      D = d0;
+      conf = 0.0;
+    } else {
+      D = d0 - FINE + arg;
+      conf = best / ((HIST_T + 1) * tot);
+    }
+  };
+  // the best split of [a, e) whose halves are both more confident than c: its boundary or -1
+  auto best_split = [&](int a, int e, double c) {
+    int bs = -1;
+    double bsum = 0.0;
+    for (int s = a + 2; s + 2 <= e && e - a >= 4; ++s) {
+      int dL, dR, nL, nR;
+      double cL, cR;
+      eval(a, s, dL, cL, nL);
+      eval(s, e, dR, cR, nR);
+      if (nL >= 2 && nR >= 2 && abs(dL - dR) >= SPLIT_MIN && cL > c && cR > c && (bs < 0 || cL + cR > bsum)) {
+        bs = s;
+        bsum = cL + cR;
+      }
+    }
+    return bs;
+  };
+  int off[4] = {0, 0, 0, 0}, dl[4] = {0, 0, 0, 0}, n = 0;
+  int D;
+  double c;
+  int nv;
+  eval(0, m, D, c, nv);
+  const int s1 = best_split(0, m, c);
+  if (s1 < 0) {
+    dl[0] = D;
+    n = 1;
+  } else {
+    const int lo[2] = {0, s1}, hi[2] = {s1, m};
+    for (int h = 0; h < 2; ++h) {  // each half once more (depth 2 ends the recursion)
+      int Dh, nh;
+      double ch;
+      eval(lo[h], hi[h], Dh, ch, nh);
+      const int s2 = best_split(lo[h], hi[h], ch);
+      if (s2 < 0) {
+        off[n] = lo[h];
+        dl[n++] = Dh;
+      } else {
+        int Da, Db, na, nb;
+        double ca, cb;
+        eval(lo[h], s2, Da, ca, na);
+        eval(s2, hi[h], Db, cb, nb);
+        off[n] = lo[h];
+        dl[n++] = Da;
+        off[n] = s2;
+        dl[n++] = Db;
+      }
+    }
+  }
+  if (tid == 0) {
+    int *o = useg + (b * MAXU + u) * USEG_P;
+    o[0] = n;
+    for (int k = 1; k < 4; ++k) o[k] = k < n ? off[k] : 0;
+    for (int k = 0; k < 4; ++k) o[4 + k] = k < n ? dl[k] : dl[0];
+  }
+}
+
+// One thread per row: the utterances' segments in order (equal neighbours merged, at most MAXSEG:
+// later ones merge into the last), the row's delay (its longest segment's, the first of equals).
+__global__ void __launch_bounds__(64) ta_segments_p862(int64_t B, int64_t L, const int32_t *__restrict__ lengths,
+                                                       const int *__restrict__ nutt, const int *__restrict__ reg,
+                                                       const int *__restrict__ useg, int *__restrict__ nseg,
+                                                       int *__restrict__ seg_start, int *__restrict__ seg_delay,
+                                                       int *__restrict__ delay) {
+  const int64_t b = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (b >= B) return;
+  const int U = nutt[b];
+  const int *rg = reg + b * (MAXU + 1);
+  int *st = seg_start + b * (MAXSEG + 1), *dl = seg_delay + b * MAXSEG;
+  int n = 0;
+  for (int u = 0; u < U; ++u) {
+    const int *o = useg + (b * MAXU + u) * USEG_P;
+    for (int k = 0; k < o[0]; ++k) {
+      const int d = o[4 + k];
+      if ((n > 0 && dl[n - 1] == d) || n == MAXSEG) continue;
+      st[n] = rg[u] + (k ? o[k] : 0) * CS;
+      dl[n] = d;
+      ++n;
+    }
+  }
+  st[n] = (int)row_len(lengths, b, L);
+  int best = -1, d = 0;
+  for (int k = 0; k < n; ++k)
+    if (st[k + 1] - st[k] > best) {
+      best = st[k + 1] - st[k];
+      d = dl[k];
+    }
+  if (nseg) nseg[b] = n;
+  if (delay) delay[b] = d;
+}
+
 inline int64_t frames_cap(int64_t L) { return L / FRAME; }
 inline int64_t nchunks(int64_t L) { return (L + CS - 1) / CS; }
 
@@ -719,6 +920,26 @@ inline UttWs utt_carve(void *ws, int64_t B, int64_t L) {
   return w;
 }
 
+// P.862 mode: the utterance-mode workspace, then the pieces' peaks and the wider segment table
+struct P862Ws {
+  float *pv;
+  int *pl, *useg;
+};
+inline size_t p862_ws_bytes(int64_t B, int64_t L) {
+  return utt_ws_bytes(B, L) + 2 * align_up((size_t)(B * nslots(L)) * 4, 256) +
+         align_up((size_t)(B * MAXU * USEG_P) * 4, 256);
+}
+inline P862Ws p862_carve(void *ws, int64_t B, int64_t L) {
+  char *p = static_cast<char *>(ws) + utt_ws_bytes(B, L);
+  P862Ws w;
+  w.pv = reinterpret_cast<float *>(p);
+  p += align_up((size_t)(B * nslots(L)) * 4, 256);
+  w.pl = reinterpret_cast<int *>(p);
+  p += align_up((size_t)(B * nslots(L)) * 4, 256);
+  w.useg = reinterpret_cast<int *>(p);
+  return w;
+}
+
 }  // namespace align
 }  // namespace fsem
 
@@ -777,11 +998,11 @@ extern "C" size_t fsem_time_align_utt_workspace_bytes(int64_t batch, int64_t len
   return align::utt_ws_bytes(batch, length);
 }
 
-extern "C" int fsem_time_align_utt_f32(const float *ref, const float *deg, int64_t batch, int64_t length,
-                                       int64_t ld, const int32_t *lengths, int32_t max_delay, int32_t *delay,
-                                       int32_t *n_seg, int32_t *seg_start, int32_t *seg_delay,
-                                       float *deg_aligned, int64_t ld_out, void *ws, size_t ws_bytes,
-                                       void *stream) {
+// the utterance and P.862 modes (stages 1-2, 5-7, then 8 or 10-12, then 9)
+static int time_align_segmented(bool p862, const float *ref, const float *deg, int64_t batch, int64_t length,
+                                int64_t ld, const int32_t *lengths, int32_t max_delay, int32_t *delay,
+                                int32_t *n_seg, int32_t *seg_start, int32_t *seg_delay, float *deg_aligned,
+                                int64_t ld_out, void *ws, size_t ws_bytes, void *stream) {
   if (!ref || !deg || batch <= 0 || length <= 0 || ld < length || length > kMaxLength || max_delay < 0 ||
       (deg_aligned && (ld_out < length || ld_out % 4 != 0)) || (ld % 4) != 0 ||
       (!delay && !n_seg && !deg_aligned) || ((n_seg != nullptr) != (seg_start != nullptr)) ||
@@ -789,7 +1010,8 @@ extern "C" int fsem_time_align_utt_f32(const float *ref, const float *deg, int64
     return FSEM_EINVAL;
   const int64_t nsl = align::nslots(length);
   if (batch * nsl > INT32_MAX) return FSEM_EINVAL;
-  if (!ws || ws_bytes < align::utt_ws_bytes(batch, length)) return FSEM_EWORKSPACE;
+  if (!ws || ws_bytes < (p862 ? align::p862_ws_bytes(batch, length) : align::utt_ws_bytes(batch, length)))
+    return FSEM_EWORKSPACE;
   hipStream_t st = (hipStream_t)stream;
   align::UttWs w = align::utt_carve(ws, batch, length);
   int *dl = delay ? delay : w.delay;
@@ -824,15 +1046,26 @@ extern "C" int fsem_time_align_utt_f32(const float *ref, const float *deg, int64
   align::ta_fine_partial<<<(unsigned)(batch * nsl), 256, 0, st>>>(
       ref, deg, batch, length, ld, lengths, w.crude, (int)nsl, w.part, align::UttTables{w.nutt, w.reg, w.cs, w.ucrude});
   FSEM_CHECK_LAUNCH();
-  {
+  if (p862) {
+    const align::P862Ws q = align::p862_carve(ws, batch, length);
+    align::ta_piece_peaks<<<(unsigned)((batch * nsl + 3) / 4), 256, 0, st>>>(batch * nsl, w.part, q.pv, q.pl);
+    FSEM_CHECK_LAUNCH();
+    dim3 grid = yz(batch);
+    grid.x = align::MAXU;
+    align::ta_pick_p862<<<grid, 256, 0, st>>>(batch, w.nutt, w.cs, w.ucrude, (int)nsl, q.pv, q.pl, q.useg);
+    FSEM_CHECK_LAUNCH();
+    align::ta_segments_p862<<<(unsigned)((batch + 63) / 64), 64, 0, st>>>(batch, length, lengths, w.nutt, w.reg,
+                                                                          q.useg, ns, ss, sd, dl);
+    FSEM_CHECK_LAUNCH();
+  } else {
     dim3 grid = yz(batch);
     grid.x = align::MAXU;
     align::ta_pick_utt<<<grid, 256, 0, st>>>(batch, w.nutt, w.cs, w.ucrude, (int)nsl, w.part, w.useg);
     FSEM_CHECK_LAUNCH();
+    align::ta_segments<<<(unsigned)((batch + 63) / 64), 64, 0, st>>>(batch, length, lengths, w.nutt, w.reg, w.useg,
+                                                                   ns, ss, sd, dl);
+    FSEM_CHECK_LAUNCH();
   }
-  align::ta_segments<<<(unsigned)((batch + 63) / 64), 64, 0, st>>>(batch, length, lengths, w.nutt, w.reg, w.useg, ns,
-                                                                 ss, sd, dl);
-  FSEM_CHECK_LAUNCH();
   if (deg_aligned) {
     dim3 grid = yz(batch);
     grid.x = (unsigned)((length + 1023) / 1024);
@@ -840,4 +1073,27 @@ extern "C" int fsem_time_align_utt_f32(const float *ref, const float *deg, int64
     FSEM_CHECK_LAUNCH();
   }
   return FSEM_OK;
+}
+
+extern "C" int fsem_time_align_utt_f32(const float *ref, const float *deg, int64_t batch, int64_t length,
+                                       int64_t ld, const int32_t *lengths, int32_t max_delay, int32_t *delay,
+                                       int32_t *n_seg, int32_t *seg_start, int32_t *seg_delay,
+                                       float *deg_aligned, int64_t ld_out, void *ws, size_t ws_bytes,
+                                       void *stream) {
+  return time_align_segmented(false, ref, deg, batch, length, ld, lengths, max_delay, delay, n_seg, seg_start,
+                              seg_delay, deg_aligned, ld_out, ws, ws_bytes, stream);
+}
+
+extern "C" size_t fsem_time_align_p862_workspace_bytes(int64_t batch, int64_t length) {
+  if (batch <= 0 || length <= 0) return 0;
+  return align::p862_ws_bytes(batch, length);
+}
+
+extern "C" int fsem_time_align_p862_f32(const float *ref, const float *deg, int64_t batch, int64_t length,
+                                        int64_t ld, const int32_t *lengths, int32_t max_delay, int32_t *delay,
+                                        int32_t *n_seg, int32_t *seg_start, int32_t *seg_delay,
+                                        float *deg_aligned, int64_t ld_out, void *ws, size_t ws_bytes,
+                                        void *stream) {
+  return time_align_segmented(true, ref, deg, batch, length, ld, lengths, max_delay, delay, n_seg, seg_start,
+                              seg_delay, deg_aligned, ld_out, ws, ws_bytes, stream);
 }

@@ -63,7 +63,7 @@ extern "C" {
 #define FSEM_ERATE -5         /* unsupported sample-rate pair (see resampling)      */
 
 const char *fsem_strerror(int code);
-int fsem_version(void);  /* 7: + fsem_host_buffer_mapped; 6: + fsem_build_id; 5: + fsem_time_align_utt_*; 4: + fsem_pre_emphasize_f32; 3: time alignment, distances */
+int fsem_version(void);  /* 8: + fsem_time_align_p862_*; 7: + fsem_host_buffer_mapped; 6: + fsem_build_id; 5: + fsem_time_align_utt_*; 4: + fsem_pre_emphasize_f32; 3: time alignment, distances */
 /* Content hash (16 hex digits) of the sources, headers and compile flags this library was built
  * from (fast_speech_enhancement_metrics_amd/_build.py source_hash); the host layer refuses a
  * library whose id differs from its own tree's.  "unknown" for builds outside _build.py. */
@@ -251,6 +251,26 @@ int fsem_time_align_utt_f32(const float *ref, const float *deg, int64_t batch, i
                             int32_t *n_seg, int32_t *seg_start, int32_t *seg_delay,
                             float *deg_aligned, int64_t ld_out, void *ws, size_t ws_bytes,
                             void *stream);
+
+/* P.862 mode (ABI 8): the utterance mode's stages up to the per-piece correlations, then P.862's
+ * histogram fine alignment and recursive utterance split (sections 10.5-10.6, restated in
+ * oracle/align_oracle.py steps 10-12 on the 5120-sample pieces instead of P.862's 64 ms frames;
+ * parity against P.862 implementations unpinned): every piece whose correlation peak reaches
+ * 5 % of its utterance's largest votes for its peak lag with weight peak^0.125; a range of
+ * pieces takes the first maximum of its triangle-smoothed (+-8 lags) vote histogram as delay and
+ * that maximum's share of the votes as confidence; a range splits at the piece boundary whose two
+ * halves (two or more votes each, delays >= 16 samples apart) are both more confident than the
+ * whole, the largest summed confidence first, and each half is tried once more (up to 4 segments
+ * per utterance; at most FSEM_ALIGN_MAX_SEGMENTS per row, later ones merging into the last).
+ * Arguments, outputs and workspace rules as fsem_time_align_utt_f32.  Replaces nothing in the
+ * reference (its PESQ has no time alignment, fast_se_metrics/PESQ.py:19-22).
+ */
+size_t fsem_time_align_p862_workspace_bytes(int64_t batch, int64_t length);
+int fsem_time_align_p862_f32(const float *ref, const float *deg, int64_t batch, int64_t length,
+                             int64_t ld, const int32_t *lengths, int32_t max_delay, int32_t *delay,
+                             int32_t *n_seg, int32_t *seg_start, int32_t *seg_delay,
+                             float *deg_aligned, int64_t ld_out, void *ws, size_t ws_bytes,
+                             void *stream);
 
 #ifdef __cplusplus
 }

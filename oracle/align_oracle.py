@@ -303,3 +303,135 @@ def align_utterances(ref: np.ndarray, deg: np.ndarray, max_delay: int = 16000, l
         out[b, :n] = shift_segments(deg[b, :n], st, dl)
         segs.append((st, dl))
     return out, ds, segs
+
+
+# ----------------------------------------------------------------------------- P.862 mode
+# Steps 1-7 as the utterance mode; then, per utterance region (P.862 sections 10.5-10.6 restated
+# on the fine stage's 320 ms pieces instead of P.862's 64 ms frames with 75 % overlap):
+#
+# 10. Piece peaks: piece i's first maximum of its first-difference correlation over the lags,
+#     (v_i, l_i) when v_i > 0 (P.862 ``time_align``: each frame's cross-correlation peak).  A
+#     piece votes when v_i >= REL_MIN times the utterance's largest piece peak: the regions
+#     include the gaps around an utterance, whose noise-only pieces would otherwise vote with
+#     weights close to the speech pieces' (the 1/8 power compresses 1e-4 to 0.32 against 1.4 for
+#     a speech piece) -- P.862 takes only the utterance's frames.
+# 11. Histogram delay of a range of pieces [a, b) (P.862 10.5): H[l] = sum of v_i^0.125 over the
+#     range's voting pieces peaking at lag l; S = H smoothed by the triangle (T + 1 - |k|),
+#     |k| <= T; the delay is the first maximum of S, its confidence S_max / ((T + 1) sum H) in
+#     (0, 1]; a range without a voting piece keeps the utterance's crude delay, confidence 0.
+# 12. Recursive split (P.862 10.6 ``utterance_split``, to depth MAXDEPTH): a range of >= 4 pieces
+#     is tried at every piece boundary s in [a + 2, b - 2]; a candidate's two halves must each hold
+#     >= 2 voting pieces, differ in delay by >= SPLIT_MIN samples and both be more confident than
+#     the whole range; the candidate with the largest summed confidence (first such s) splits the
+#     range and each half is tried again.  Up to 2^MAXDEPTH segments per utterance, in order; the row's segments are the
+#     utterances' in order, equal neighbours merged, at most MAXSEG (later ones merge into the
+#     last); the row's delay is its longest segment's (the first of equals).
+HIST_T = 8        # lags: half-width of the histogram's triangular smoothing (0.5 ms)
+HIST_POW = 0.125  # weight of a piece: its correlation peak to this power (P.862)
+REL_MIN = 0.05    # a piece votes from this fraction of the utterance's largest piece peak
+MAXDEPTH = 2
+
+
+def piece_peaks(P: np.ndarray):
+    """Step 10: ([m] peak values, [m] peak lag indices; -1 where the piece does not vote)."""
+    v = np.zeros(P.shape[0])
+    idx = np.full(P.shape[0], -1, dtype=np.int64)
+    for i in range(P.shape[0]):
+        j = int(np.argmax(P[i]))
+        if P[i, j] > 0:
+            v[i], idx[i] = P[i, j], j
+    vmax = v.max() if v.size else 0.0
+    idx[v < REL_MIN * vmax] = -1
+    return v, idx
+
+
+def hist_delay(v: np.ndarray, idx: np.ndarray, a: int, b: int, d0: int):
+    """Step 11: (delay, confidence, voting pieces) of pieces [a, b)."""
+    H = np.zeros(2 * FINE + 1)
+    nv = 0
+    for i in range(a, b):
+        if idx[i] >= 0:
+            H[idx[i]] += v[i] ** HIST_POW
+            nv += 1
+    tot = H.sum()
+    if nv == 0:
+        return d0, 0.0, 0
+    S = np.zeros_like(H)
+    for k in range(-HIST_T, HIST_T + 1):
+        w = HIST_T + 1 - abs(k)
+        if k >= 0:
+            S[:H.shape[0] - k] += w * H[k:]
+        else:
+            S[-k:] += w * H[:H.shape[0] + k]
+    j = int(np.argmax(S))
+    return d0 - FINE + j, float(S[j] / ((HIST_T + 1) * tot)), nv
+
+
+def split_p862(v, idx, a: int, b: int, d0: int, depth: int = 0) -> list:
+    """Step 12: [(piece offset from a, delay)] of pieces [a, b)."""
+    D, c, _ = hist_delay(v, idx, a, b, d0)
+    if depth < MAXDEPTH and b - a >= 4:
+        best = None
+        for s in range(a + 2, b - 1):
+            if b - s < 2:
+                break
+            dL, cL, nL = hist_delay(v, idx, a, s, d0)
+            dR, cR, nR = hist_delay(v, idx, s, b, d0)
+            if (nL >= 2 and nR >= 2 and abs(dL - dR) >= SPLIT_MIN and cL > c and cR > c
+                    and (best is None or cL + cR > best[0])):
+                best = (cL + cR, s)
+        if best is not None:
+            s = best[1]
+            return (split_p862(v, idx, a, s, d0, depth + 1) +
+                    [(s - a + o, d) for o, d in split_p862(v, idx, s, b, d0, depth + 1)])
+    return [(0, D)]
+
+
+def segments_p862(ref: np.ndarray, deg: np.ndarray, max_delay: int = 16000):
+    """(seg_start [n+1], seg_delay [n], row delay) of one row pair (steps 5-7, 10-12)."""
+    r = np.asarray(ref, dtype=np.float64)
+    d = np.asarray(deg, dtype=np.float64)
+    L = r.shape[0]
+    env_r, env_d = envelope(r), envelope(d)
+    nfr = env_r.shape[0]
+    M = min(-(-max_delay // FRAME), nfr - 1) if nfr >= 2 else 0
+    jrow = crude_delay(env_r, env_d, -(-max_delay // FRAME)) if nfr >= 2 else 0
+    utt = utterances(env_r)
+    R = region_starts(utt, L)
+    wr = np.zeros(L)
+    wd = np.zeros(L)
+    wr[1:] = np.diff(r)
+    wd[1:] = np.diff(d)
+    starts, delays = [], []
+    wins = utt if utt else [(0, nfr)]
+    for u, (s, e) in enumerate(wins):
+        j = crude_window(env_r, env_d, max(0, s - SEARCHBUF), min(nfr, e + SEARCHBUF),
+                         max(-M, jrow - SEARCHBUF), min(M, jrow + SEARCHBUF))
+        d0 = FRAME * (j if j is not None else jrow)
+        v, idx = piece_peaks(fine_pieces(wr, wd, R[u], R[u + 1], d0))
+        for off, D in split_p862(v, idx, 0, v.shape[0], d0):
+            if delays and delays[-1] == D:
+                continue  # merged with the previous segment
+            if len(delays) == MAXSEG:
+                continue  # the row's segment table is full: the last segment runs on
+            starts.append(R[u] + off * CHUNK)
+            delays.append(D)
+    starts.append(L)
+    lens = np.diff(starts)
+    return np.array(starts), np.array(delays), int(delays[int(np.argmax(lens))])
+
+
+def align_p862(ref: np.ndarray, deg: np.ndarray, max_delay: int = 16000, lengths=None):
+    """(aligned [B, L], row delays [B], [(seg_start, seg_delay)] per row) for [B, L] rows."""
+    ref = np.atleast_2d(ref)
+    deg = np.atleast_2d(deg)
+    B, L = ref.shape
+    out = np.zeros_like(deg)
+    ds = np.zeros(B, dtype=np.int64)
+    segs = []
+    for b in range(B):
+        n = L if lengths is None else int(min(max(lengths[b], 0), L))
+        st, dl, ds[b] = segments_p862(ref[b, :n], deg[b, :n], max_delay)
+        out[b, :n] = shift_segments(deg[b, :n], st, dl)
+        segs.append((st, dl))
+    return out, ds, segs

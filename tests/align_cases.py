@@ -58,3 +58,26 @@ def batch(seed0: int = 5):
     """[B, L_UTT] clean / degraded rows of CASES (seeds seed0, seed0 + 1, ...)."""
     rows = [utt_pair(seed0 + i, L_UTT, u, d, sp) for i, (u, d, sp, _) in enumerate(CASES)]
     return np.stack([r[0] for r in rows]), np.stack([r[1] for r in rows])
+
+
+def continuous_pair(seed: int, L: int, pieces):
+    """(clean, degraded) float32 rows of one continuous utterance (amplitude-modulated coloured
+    noise: no gap the voice-activity envelope would cut) whose degraded row is shifted by
+    pieces = [(start, end, D)]: several delays inside ONE utterance (the P.862 mode's recursive
+    split)."""
+    rng = np.random.default_rng(seed)
+    t = np.arange(L) / 16000
+    x = np.convolve(rng.standard_normal(L + 64), np.hanning(9), "same")[:L]
+    c = x * (1.2 + np.sin(2 * np.pi * 4.3 * t) + 0.5 * np.sin(2 * np.pi * 2.1 * t + 1))
+    n = c + 0.05 * rng.standard_normal(L)
+    deg = 1e-3 * rng.standard_normal(L)
+    for a, b, D in pieces:
+        seg = np.zeros(L)
+        seg[a:b] = n[a:b]
+        deg += _shift(seg, D)
+    return c.astype(np.float32), deg.astype(np.float32)
+
+
+# one utterance, three delays: two levels of the P.862 mode's split
+L_CONT = 128000
+CONT_PIECES = [(0, 40000, 100), (40000, 85000, 400), (85000, L_CONT, -200)]
