@@ -19,13 +19,13 @@ from .spectrogram import Spectrogram
 def _unit_rows(x: torch.Tensor, lengths=None) -> torch.Tensor:
     """Rows scaled by a power of two (exact) to a peak in [1, 2) of their first lengths[b] samples;
     zero / non-finite rows as they are."""
-    a = x.abs()
+    a = x
     if lengths is not None:
         t = torch.arange(x.shape[1], device=x.device)
-        a = torch.where(t[None, :] < torch.as_tensor(lengths, device=x.device).reshape(-1, 1), a, torch.zeros_like(a))
-    peak = a.amax(dim=1)
+        a = x.masked_fill(t[None, :] >= torch.as_tensor(lengths, device=x.device).reshape(-1, 1), 0.0)
+    peak = torch.linalg.vector_norm(a, ord=float("inf"), dim=1)  # max |x|: one pass over the rows
     ex = torch.where((peak > 0) & torch.isfinite(peak), torch.floor(torch.log2(peak)), torch.zeros_like(peak))
-    return torch.ldexp(x, -ex[:, None].to(x.dtype))
+    return x * torch.exp2(-ex).to(x.dtype)[:, None]  # a power of two: exact, as ldexp
 
 
 class PESQ(BaseMetric):
@@ -279,6 +279,9 @@ class PESQ(BaseMetric):
         B, L = clean.shape
         if noisy.shape != clean.shape:
             raise Exception("`clean_speech` and `denoised_speech` should have the same shape.")
+        if getattr(self, "time_align", False) == "p862":
+            mos, delays, _, _ = self.p862_scores(clean, noisy, lengths)
+            return mos, delays
         if getattr(self, "time_align", False):
             from .alignment import time_align
             noisy, delays = time_align(clean, noisy, lengths, self.max_delay, mode=self.time_align)
@@ -304,6 +307,40 @@ class PESQ(BaseMetric):
                                            mos.data_ptr(), ws.data_ptr(), ws.numel(),
                                            _native.stream_handle(clean.device)), "PESQ")
         return mos, delays
+
+    def p862_scores(self, clean_speech: torch.Tensor, noisy_speech: torch.Tensor, lengths=None):
+        """The ``time_align="p862"`` scores of 16 kHz rows (extension, not in the reference,
+        PESQ.py:19-22): the P.862-mode alignment (``alignment.time_align_segments``), the aligned
+        rows' per-frame disturbances, P.862's realignment of bad intervals
+        (``alignment.realign_bad_intervals``), the realigned rows' disturbances (only rows with an
+        interval), and the MOS of the frames each interval scores better with
+        (``fsem_pesq_pool_f32``).  Returns (mos [B] float32, delays [B], n_bad [B], bad [B, 16, 3])
+        on the rows' device (CPU rows: _cpu.pesq_p862, mos float64)."""
+        from . import alignment
+        clean = as_rows(clean_speech)
+        noisy = as_rows(noisy_speech)
+        B, L = clean.shape
+        max_delay = getattr(self, "max_delay", alignment.DEFAULT_MAX_DELAY)
+        if not clean.is_cuda:
+            lens = None if lengths is None else device_lengths(lengths, B, L, "cpu")
+            return _cpu.pesq_p862(clean, noisy, lens, max_delay)
+        lib = _native.load()
+        lens = device_lengths(lengths, B, L, clean.device) if lengths is not None else None
+        aligned, delays, nseg, starts, sdel = alignment.time_align_segments(clean, noisy, lens, max_delay, mode="p862")
+        ds, _, fr1 = self.frame_disturbances(clean, aligned, lens)
+        n_bad, bad, second = alignment.realign_bad_intervals(clean, noisy, aligned, fr1, nseg, starts, sdel, lens)
+        fr2 = fr1
+        rows = torch.nonzero(n_bad).flatten()  # host sync: the second scoring covers these rows only
+        if rows.numel():
+            fr2 = fr1.clone()
+            _, _, sub = self.frame_disturbances(clean[rows], second[rows], None if lens is None else lens[rows])
+            fr2[rows] = sub
+        mos = torch.empty(B, dtype=torch.float32, device=clean.device)
+        _native.check(lib.fsem_pesq_pool_f32(fr1.data_ptr(), fr2.data_ptr(), ds.data_ptr(), B, L,
+                                             lens.data_ptr() if lens is not None else None, n_bad.data_ptr(),
+                                             bad.data_ptr(), mos.data_ptr(), _native.stream_handle(clean.device)),
+                      "PESQ pool")
+        return mos, delays, n_bad, bad
 
     def compute_metric(self, clean_speech: torch.Tensor | None, denoised_speech: torch.Tensor,
                        lengths=None) -> list[dict[str, float]]:

@@ -565,3 +565,101 @@ def time_align(clean: torch.Tensor, noisy: torch.Tensor, lengths=None, max_delay
         if hi > lo:
             out[b, lo:hi] = n[b, lo + D:hi + D]
     return torch.from_numpy(out), torch.from_numpy(ds)
+
+
+# bad intervals (csrc/align.hip ta_bad_*; P.862 section 10.7): the P.862 mode's realignment of
+# runs of badly scored frames, then the pooling over the better-scored frames
+_BAD_THR, _BAD_GAP, _BAD_MIN, _BAD_MAX, _HOP = 30.0, 4, 5, 16, 256
+
+
+def bad_runs(sym: np.ndarray) -> list:
+    """[(f0, f1)]: runs of frames above BAD_THR, joined across gaps < BAD_GAP, from BAD_MIN
+    frames, at most BAD_MAX in order."""
+    bad = np.flatnonzero(np.asarray(sym) > _BAD_THR)
+    if bad.size == 0:
+        return []
+    cut = np.flatnonzero(np.diff(bad) > 1)
+    rs = np.concatenate([[bad[0]], bad[cut + 1]])
+    re = np.concatenate([bad[cut] + 1, [bad[-1] + 1]])
+    j = np.flatnonzero(rs[1:] - re[:-1] >= _BAD_GAP)
+    s = np.concatenate([[rs[0]], rs[j + 1]])
+    e = np.concatenate([re[j], [re[-1]]])
+    return [(int(a), int(b)) for a, b in zip(s, e) if b - a >= _BAD_MIN][:_BAD_MAX]
+
+
+def pesq_frame_scores(clean: torch.Tensor, noisy: torch.Tensor):
+    """Per-frame (symmetric, asymmetric) disturbances [B, F] of [B, L] 16 kHz rows."""
+    B = clean.shape[0]
+    bark = bark_of_rows(torch.cat([clean, noisy], 0))
+    ec, en = equalize(bark[:B], bark[B:])
+    return frame_disturbances(ec, en)
+
+
+def realign_bad_row(ref: np.ndarray, deg: np.ndarray, aligned: np.ndarray, starts, delays, sym: np.ndarray):
+    """([(f0, f1, delay)], second degraded row) of one unpadded row."""
+    L = deg.shape[0]
+    out = np.array(aligned, dtype=np.float32, copy=True)
+    runs = bad_runs(sym)
+    if not runs:
+        return [], out
+    wr = np.zeros(L)
+    wd = np.zeros(L)
+    wr[1:] = np.diff(np.asarray(ref, dtype=np.float64))
+    wd[1:] = np.diff(np.asarray(deg, dtype=np.float64))
+    res = []
+    for f0, f1 in runs:
+        a, e = _HOP * f0, min(_HOP * f1 + _HOP, L)
+        k = int(np.searchsorted(starts, a, side="right")) - 1
+        d0 = int(delays[min(max(k, 0), len(delays) - 1)])
+        i = _first_max(_ta_piece_xcorr(wr, wd, a, e, d0 - _TA_FINE, d0 + _TA_FINE))
+        D = d0 - _TA_FINE + i if i >= 0 else d0
+        res.append((f0, f1, D))
+        lo, hi = max(a, -D), min(e, L - D)
+        out[a:e] = 0.0
+        if hi > lo:
+            out[lo:hi] = deg[lo + D:hi + D]
+    return res, out
+
+
+def pesq_p862_row(ref: np.ndarray, deg: np.ndarray, aligned: np.ndarray, starts, delays):
+    """(MOS, [(f0, f1, delay)]) of one unpadded row already aligned by the P.862 mode."""
+    L = ref.shape[0]
+    if pesq_frames(L) < 20:
+        return float("nan"), []
+    c = torch.from_numpy(np.ascontiguousarray(ref, dtype=np.float32)).unsqueeze(0)
+    s1, a1 = pesq_frame_scores(c, torch.from_numpy(np.ascontiguousarray(aligned, dtype=np.float32)).unsqueeze(0))
+    res, second = realign_bad_row(ref, deg, aligned, starts, delays, s1[0].numpy())
+    if res:
+        s2, a2 = pesq_frame_scores(c, torch.from_numpy(second).unsqueeze(0))
+        s1, a1 = s1.clone(), a1.clone()
+        for f0, f1, _ in res:
+            if float(s2[0, f0:f1].sum()) < float(s1[0, f0:f1].sum()):
+                s1[0, f0:f1] = s2[0, f0:f1]
+                a1[0, f0:f1] = a2[0, f0:f1]
+    return float(mos_of(overlapping_sums(s1), overlapping_sums(a1))[0]), res
+
+
+def pesq_p862(clean: torch.Tensor, noisy: torch.Tensor, lengths=None, max_delay: int = 16000):
+    """(MOS [B] float64, delays [B] int32, n_bad [B] int32, bad [B, 16, 3] int32) of 16 kHz rows:
+    the P.862-mode alignment, then the bad-interval realignment."""
+    aligned, ds, ns, st, sd = time_align_utterances(clean, noisy, lengths, max_delay, mode="p862")
+    c = clean.detach().cpu().float().numpy()
+    n = noisy.detach().cpu().float().numpy()
+    a = aligned.numpy()
+    B, L = c.shape
+    rows = [L if lengths is None else int(min(max(int(lengths[b]), 0), L)) for b in range(B)]
+
+    def one(b):
+        k = int(ns[b])
+        m = rows[b]
+        return pesq_p862_row(c[b, :m], n[b, :m], a[b, :m], st[b, :k + 1].numpy(), sd[b, :k].numpy())
+
+    res = _host_map(one, range(B))
+    mos = torch.tensor([r[0] for r in res], dtype=torch.float64)
+    nb = torch.zeros(B, dtype=torch.int32)
+    bad = torch.zeros(B, _BAD_MAX, 3, dtype=torch.int32)
+    for b, (_, iv) in enumerate(res):
+        nb[b] = len(iv)
+        if iv:
+            bad[b, :len(iv)] = torch.tensor(iv, dtype=torch.int32)
+    return mos, ds, nb, bad

@@ -67,8 +67,13 @@ SIGNATURES = {
                                                  _vp, _c_i64, _vp, _c_sz, _vp]),
     "fsem_time_align_utt_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _c_i32, _vp, _vp, _vp, _vp,
                                                 _vp, _c_i64, _vp, _c_sz, _vp]),
+    "fsem_pesq_bad_intervals_workspace_bytes": (_c_sz, [_c_i64, _c_i64]),
+    "fsem_pesq_bad_intervals_f32": (ctypes.c_int, [_vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp,
+                                                    _vp, _vp, _vp, _c_i64, _vp, _c_sz, _vp]),
+    "fsem_pesq_pool_f32": (ctypes.c_int, [_vp, _vp, _vp, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp]),
 }
 ALIGN_MAX_SEGMENTS = 32  # include/fsem.h FSEM_ALIGN_MAX_SEGMENTS
+PESQ_MAX_BAD = 16  # include/fsem.h FSEM_PESQ_MAX_BAD
 
 
 _score_list_mod = None  # the native builder's module; False: unavailable, the Python form is used

@@ -134,3 +134,45 @@ def time_align_segments(clean: torch.Tensor, noisy: torch.Tensor, lengths=None,
                         out.data_ptr(), out.stride(0), ws.data_ptr(), ws.numel(), _native.stream_handle(c.device)),
                   "time alignment")
     return out, delays, nseg, starts, sdel
+
+
+def realign_bad_intervals(clean: torch.Tensor, noisy: torch.Tensor, aligned: torch.Tensor, frames: torch.Tensor,
+                          n_seg: torch.Tensor, seg_start: torch.Tensor, seg_delay: torch.Tensor, lengths=None):
+    """P.862's realignment of bad intervals (section 10.7; ``fsem_pesq_bad_intervals_f32``) of
+    16 kHz rows on the GPU, after ``time_align_segments(..., mode="p862")`` and the aligned rows'
+    per-frame disturbances (``PESQ.frame_disturbances``, [B, 2, F]).
+
+    Returns (n_bad [B], bad [B, 16, 3], second [B, L]) on the rows' device: row b's intervals
+    bad[b, i] = (first frame, end frame, delay) for i < n_bad[b] -- runs of frames whose symmetric
+    disturbance exceeds 30, joined across gaps under 4 frames, from 5 frames long -- each with the
+    delay of the first-difference correlation's first maximum over its samples [256 f0,
+    256 f1 + 256) within +-383 of its segment's delay; ``second`` is ``aligned`` with those
+    samples taken at the interval's delay instead.
+    """
+    c, n, _ = _prepare(clean, noisy, 0)
+    if not c.is_cuda:
+        raise RuntimeError("realign_bad_intervals: GPU rows only (the CPU path is _cpu.pesq_p862)")
+    B, L = c.shape
+    lib = _native.load()
+    lens = device_lengths(lengths, B, L, c.device) if lengths is not None else None
+    c, n = _device_rows(c, n)
+    F = lib.fsem_pesq_frames(L)
+    frames = frames.float().contiguous()
+    if tuple(frames.shape) != (B, 2, F):
+        raise ValueError(f"frames must be [B, 2, {F}]")
+    a = aligned.float()
+    if a.stride(1) != 1 or a.stride(0) % 4 or a.data_ptr() % 16 or a.shape != (B, L):
+        a = torch.nn.functional.pad(a.contiguous(), (0, (-L) % 4))[:, :L]
+    second = torch.empty(B, a.stride(0), dtype=torch.float32, device=c.device)[:, :L]
+    i32 = dict(dtype=torch.int32, device=c.device)
+    n_bad = torch.empty(B, **i32)
+    bad = torch.zeros(B, _native.PESQ_MAX_BAD, 3, **i32)
+    segs = [t.to(**i32).contiguous() for t in (n_seg, seg_start, seg_delay)]
+    ws = _native.workspace(lib.fsem_pesq_bad_intervals_workspace_bytes(B, L), c.device)
+    _native.check(lib.fsem_pesq_bad_intervals_f32(c.data_ptr(), n.data_ptr(), a.data_ptr(), B, L, c.stride(0),
+                                                  lens.data_ptr() if lens is not None else None, frames.data_ptr(),
+                                                  segs[0].data_ptr(), segs[1].data_ptr(), segs[2].data_ptr(),
+                                                  n_bad.data_ptr(), bad.data_ptr(), second.data_ptr(), a.stride(0),
+                                                  ws.data_ptr(), ws.numel(), _native.stream_handle(c.device)),
+                  "bad-interval realignment")
+    return n_bad, bad, second

@@ -211,11 +211,15 @@ static_assert(kFineLds <= 80 * 1024, "ta_fine_partial: two workgroups per CU in 
 // Utterance mode (utt != nullptr): slot c of row b is piece i of utterance u (pieces of u are
 // slots [cs[u], cs[u+1])): samples [reg[u] + i CS, min(reg[u] + (i+1) CS, reg[u+1])) at lags
 // around that utterance's crude delay (ucrude[u]).
+// Bad-interval realignment (desc != nullptr): slot c < ndesc[b] of row b is desc[b][c] = {first
+// sample, end sample, centre lag, interval}.
 struct UttTables {
   const int *nutt;    // [B]
   const int *reg;     // [B][MAXU + 1] region starts (samples)
   const int *cs;      // [B][MAXU + 1] first piece slot per utterance
   const int *ucrude;  // [B][MAXU] crude delay (samples)
+  const int4 *desc = nullptr;
+  const int *ndesc = nullptr;  // [B]
 };
 __global__ void __launch_bounds__(256) ta_fine_partial(const float *__restrict__ ref, const float *__restrict__ deg,
                                                        int64_t B, int64_t L, int64_t ld,
@@ -226,12 +230,14 @@ __global__ void __launch_bounds__(256) ta_fine_partial(const float *__restrict__
   __shared__ float wd[WIN + WIN / 32 + 64];
   __shared__ float ps[NSL][NGRP * LG];
   const int64_t blk = blockIdx.x;
-  const int64_t b = blk / nchunk;
-  const int c = (int)(blk % nchunk);
+  // slot descriptors (few active slots per row): rows fastest, so the active workgroups spread
+  // over the XCDs instead of landing on the few that row-major slot ids map to
+  const int64_t b = ut.desc ? blk % B : blk / nchunk;
+  const int c = (int)(ut.desc ? blk / B : blk % nchunk);
   if (b >= B) return;
   const int64_t Lr = row_len(lengths, b, L);
   int64_t n0 = (int64_t)c * CS, hi = n0 + CS;
-  int64_t lag0 = (int64_t)crude[b] - FINE;
+  int64_t lag0 = crude ? (int64_t)crude[b] - FINE : 0;  // crude: NULL with slot descriptors
   if (ut.nutt) {
     const int U = ut.nutt[b];
     const int *cs = ut.cs + b * (MAXU + 1);
@@ -242,6 +248,12 @@ __global__ void __launch_bounds__(256) ta_fine_partial(const float *__restrict__
     n0 = (int64_t)reg[u] + (int64_t)(c - cs[u]) * CS;
     hi = std::min<int64_t>(n0 + CS, reg[u + 1]);
     lag0 = (int64_t)ut.ucrude[b * MAXU + u] - FINE;
+  } else if (ut.desc) {
+    if (c >= ut.ndesc[b]) return;  // past the row's pieces (uniform)
+    const int4 d = ut.desc[b * nchunk + c];
+    n0 = d.x;
+    hi = d.y;
+    lag0 = (int64_t)d.z - FINE;
   }
   const float *x = ref + b * ld, *y = deg + b * ld;
   const int tid = threadIdx.x;
@@ -480,14 +492,18 @@ __device__ __forceinline__ void block_argmax(double &v, int &j, double *sv, int 
 // ---------------------------------------------------------------- stage 6: per-utterance crude
 // Workgroup (utterance u, row b): lag j = jrow - SEARCHBUF + tid (within |j| <= M), the envelope
 // correlation over reference frames [start - SEARCHBUF, end + SEARCHBUF), k ascending in float.
+// The window's frames of both envelopes are staged in LDS when they fit (UTT_LDS each; longer
+// utterances read global memory): each lane's chain of fmaf then waits on LDS, not on HBM.
+constexpr int UTT_LDS = 4096;
 __global__ void __launch_bounds__(256) ta_crude_utt(int64_t B, int64_t L, const int32_t *__restrict__ lengths,
                                                     const float *__restrict__ E, int64_t nfr_cap, int max_frames,
                                                     const int *__restrict__ crude, const int *__restrict__ nutt,
                                                     const int *__restrict__ utt, int *__restrict__ ucrude) {
   __shared__ double sv[4];
   __shared__ int sj[4];
-  const int u = blockIdx.x;
-  const int64_t b = blockIdx.y + (int64_t)blockIdx.z * 65535;
+  __shared__ float sr[UTT_LDS], sd[UTT_LDS + 2 * SEARCHBUF + 1];
+  const int u = blockIdx.y;  // rows fastest in the dispatch order: a row's active workgroups spread over the XCDs
+  const int64_t b = blockIdx.x + (int64_t)blockIdx.z * 65535;
   if (b >= B || u >= nutt[b]) return;
   const int nfr = (int)(row_len(lengths, b, L) / FRAME);
   const int M = nfr < 2 ? 0 : min(max_frames, nfr - 1);
@@ -495,14 +511,34 @@ __global__ void __launch_bounds__(256) ta_crude_utt(int64_t B, int64_t L, const 
   const int jlo = max(-M, jrow - SEARCHBUF), jhi = min(M, jrow + SEARCHBUF);
   const int k0 = max(0, utt[b * 2 * MAXU + 2 * u] - SEARCHBUF);
   const int k1 = min(nfr, utt[b * 2 * MAXU + 2 * u + 1] + SEARCHBUF);
-  const float *r = E + b * nfr_cap, *d = E + (B + b) * nfr_cap;
+  const float *gr = E + b * nfr_cap, *gd = E + (B + b) * nfr_cap;
+  // LDS: sr[k - k0] = r[k] for k in [k0, k1); sd[m - k0 - jlo] = d[m] for m in [k0 + jlo, k1 + jhi)
+  // (frames outside [0, nfr) are never read: ks / ke clip every lag's range)
+  const bool in_lds = k1 - k0 <= UTT_LDS && jhi - jlo <= 2 * SEARCHBUF;
+  if (in_lds) {
+    for (int k = (int)threadIdx.x; k < k1 - k0; k += 256) sr[k] = gr[k0 + k];
+    for (int k = (int)threadIdx.x; k < k1 - k0 + jhi - jlo; k += 256) {
+      const int m = k0 + jlo + k;
+      sd[k] = (m >= 0 && m < nfr) ? gd[m] : 0.f;
+    }
+  }
+  __syncthreads();
   const int j = jlo + (int)threadIdx.x;
   double best = 0.0;
   int arg = INT32_MAX;
   if (j <= jhi) {
     const int ks = max(k0, -j), ke = min(k1, nfr - j);
     float c = 0.f;
-    for (int k = ks; k < ke; ++k) c = fmaf(r[k], d[k + j], c);
+    // two loops, not one over a selected pointer: a generic pointer turns the LDS reads into flat
+    // loads (and one offset below the LDS aperture faults); index offsets, k ascending either way
+    // (unrolled by 8: eight loads in flight per wait, the chain of fmaf in the same order)
+    if (in_lds) {
+#pragma unroll 8
+      for (int k = ks; k < ke; ++k) c = fmaf(sr[k - k0], sd[k + j - k0 - jlo], c);
+    } else {
+#pragma unroll 8
+      for (int k = ks; k < ke; ++k) c = fmaf(gr[k], gd[k + j], c);
+    }
     if (c > 0.f) {
       best = c;
       arg = j;
@@ -522,8 +558,8 @@ __global__ void __launch_bounds__(256) ta_pick_utt(int64_t B, const int *__restr
                                                    const float *__restrict__ part, int *__restrict__ useg) {
   __shared__ double sv[4];
   __shared__ int sj[4];
-  const int u = blockIdx.x;
-  const int64_t b = blockIdx.y + (int64_t)blockIdx.z * 65535;
+  const int u = blockIdx.y;  // rows fastest in the dispatch order: a row's active workgroups spread over the XCDs
+  const int64_t b = blockIdx.x + (int64_t)blockIdx.z * 65535;
   if (b >= B || u >= nutt[b]) return;
   const int tid = threadIdx.x;
   const int c0 = cs[b * (MAXU + 1) + u], m = cs[b * (MAXU + 1) + u + 1] - c0;
@@ -670,7 +706,8 @@ constexpr int USEG_P = 8;            // per utterance: {segments, 3 piece offset
 // One wave per piece slot: the first maximum above zero of its NLAG partials, (value, lag index),
 // or (0, -1).  Keys (value bits, ~lag) order positive floats as values, ties to the smaller lag.
 __global__ void __launch_bounds__(256) ta_piece_peaks(int64_t nslot_total, const float *__restrict__ part,
-                                                      float *__restrict__ pv, int *__restrict__ pl) {
+                                                      float *__restrict__ pv, int *__restrict__ pl,
+                                                      double *__restrict__ pw) {
   const int64_t slot = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (slot >= nslot_total) return;  // wave-uniform
   const int lane = threadIdx.x & 63;
@@ -690,26 +727,33 @@ __global__ void __launch_bounds__(256) ta_piece_peaks(int64_t nslot_total, const
   if (lane == 0) {
     pv[slot] = key ? __uint_as_float((unsigned)(key >> 32)) : 0.f;
     pl[slot] = key ? (int)(0xFFFFFFFFu - (unsigned)key) : -1;
+    pw[slot] = key ? pow((double)__uint_as_float((unsigned)(key >> 32)), HIST_POW) : 0.0;  // its vote
   }
 }
 
 // Workgroup (utterance u, row b): its m pieces' peaks, the votes (REL_MIN of the largest), then
-// up to three range evaluations' split searches (stage 12).  A range's histogram is rebuilt from
-// its pieces for every evaluation, each lag's votes added in piece order (double).
+// up to three range evaluations' split searches (stage 12).  The votes (lag, peak^0.125) are
+// computed once into LDS (utterances up to PCACHE pieces, 175 minutes at 16 kHz; longer ones
+// recompute them from global memory per evaluation); a range's histogram is rebuilt from its
+// pieces for every evaluation, each lag's votes and the total added in piece order (double).
+constexpr int PCACHE = 2048;
 __global__ void __launch_bounds__(256) ta_pick_p862(int64_t B, const int *__restrict__ nutt, const int *__restrict__ cs,
                                                     const int *__restrict__ ucrude, int nslot,
                                                     const float *__restrict__ pv, const int *__restrict__ pl,
-                                                    int *__restrict__ useg) {
+                                                    const double *__restrict__ pwg, int *__restrict__ useg) {
   __shared__ double sv[4];
   __shared__ int sj[4];
   __shared__ double H[NGRP * LG + 2 * HIST_T];  // lag l at H[HIST_T + l]; zero margins
-  const int u = blockIdx.x;
-  const int64_t b = blockIdx.y + (int64_t)blockIdx.z * 65535;
+  __shared__ double pw[PCACHE];                 // a piece's vote, 0 if it does not vote
+  __shared__ int pg[PCACHE];                    // its lag index, -1 if it does not vote
+  const int u = blockIdx.y;  // rows fastest in the dispatch order: a row's active workgroups spread over the XCDs
+  const int64_t b = blockIdx.x + (int64_t)blockIdx.z * 65535;
   if (b >= B || u >= nutt[b]) return;
   const int tid = threadIdx.x;
   const int c0 = cs[b * (MAXU + 1) + u], m = cs[b * (MAXU + 1) + u + 1] - c0;
   const float *v = pv + b * nslot + c0;
   const int *lg = pl + b * nslot + c0;
+  const double *vw = pwg + b * nslot + c0;
   const int d0 = ucrude[b * MAXU + u];
   // the utterance's largest piece peak
   double vmax = 0.0;
@@ -719,26 +763,46 @@ __global__ void __launch_bounds__(256) ta_pick_p862(int64_t B, const int *__rest
     block_argmax(vmax, dummy, sv, sj);
   }
   const double vmin = REL_MIN * vmax;
-  auto votes = [&](int i) { return lg[i] >= 0 && (double)v[i] >= vmin; };
+  const bool cached = m <= PCACHE;
+  auto vote = [&](int i, int &l, double &w) {  // piece i's lag index (-1: no vote) and weight
+    if (cached) {
+      l = pg[i];
+      w = pw[i];
+    } else {
+      const bool ok = lg[i] >= 0 && (double)v[i] >= vmin;
+      l = ok ? lg[i] : -1;
+      w = ok ? vw[i] : 0.0;  // no pow here: a select would evaluate it for every piece
+    }
+  };
+  if (cached)
+    for (int i = tid; i < m; i += 256) {
+      const bool ok = lg[i] >= 0 && (double)v[i] >= vmin;
+      pg[i] = ok ? lg[i] : -1;
+      pw[i] = ok ? vw[i] : 0.0;
+    }
+  for (int l = tid; l < NGRP * LG + 2 * HIST_T; l += 256)
+    if (l < HIST_T || l >= HIST_T + NLAG) H[l] = 0.0;  // the margins, once: evaluations write every lag
   // (delay, confidence, votes) of pieces [a, e): every thread the same values
   auto eval = [&](int a, int e, int &D, double &conf, int &nv) {
-    __syncthreads();  // the previous evaluation's readers of H are done
-    for (int l = tid; l < NGRP * LG + 2 * HIST_T; l += 256) H[l] = 0.0;
-    __syncthreads();
+    __syncthreads();  // the previous evaluation's readers of H (and the LDS fills above) are done
     int cnt = 0;
-    double h[3] = {0.0, 0.0, 0.0};
-    for (int i = a; i < e; ++i) {  // piece order; the thread's own lags only
-      if (!votes(i)) continue;
-      ++cnt;
-      const int l = lg[i];
-      if ((l & 255) == tid) h[l >> 8] += pow((double)v[i], HIST_POW);
+    double tot = 0.0, h[3] = {0.0, 0.0, 0.0};
+#pragma unroll 4
+    for (int i = a; i < e; ++i) {  // piece order; the thread's own lags only (branch-free: + 0.0)
+      int l;
+      double w;
+      vote(i, l, w);
+      cnt += l >= 0;
+      tot += w;  // w = 0 for a piece that does not vote
+      const double add = ((l & 255) == tid) ? w : 0.0;  // selects, not h[l >> 8]: no scratch array
+      h[0] += (l >> 8) == 0 ? add : 0.0;
+      h[1] += (l >> 8) == 1 ? add : 0.0;
+      h[2] += (l >> 8) == 2 ? add : 0.0;
     }
 #pragma unroll
     for (int q = 0; q < 3; ++q)
       if (tid + 256 * q < NLAG) H[HIST_T + tid + 256 * q] = h[q];
     __syncthreads();
-    double tot = 0.0;
-    for (int l = 0; l < NLAG; ++l) tot += H[HIST_T + l];  // lag order (every thread)
     double best = -1.0;
     int arg = INT32_MAX;
 #pragma unroll
@@ -763,51 +827,52 @@ __global__ void __launch_bounds__(256) ta_pick_p862(int64_t B, const int *__rest
       conf = best / ((HIST_T + 1) * tot);
     }
   };
-  // the best split of [a, e) whose halves are both more confident than c: its boundary or -1
+  // the best split of [a, e) whose halves are both more confident than c: its boundary or -1.
+  // One evaluation call site (left half at even t, right half at odd t): the evaluation is
+  // inlined twice in the kernel, not once per use.
   auto best_split = [&](int a, int e, double c) {
-    int bs = -1;
-    double bsum = 0.0;
-    for (int s = a + 2; s + 2 <= e && e - a >= 4; ++s) {
-      int dL, dR, nL, nR;
-      double cL, cR;
-      eval(a, s, dL, cL, nL);
-      eval(s, e, dR, cR, nR);
-      if (nL >= 2 && nR >= 2 && abs(dL - dR) >= SPLIT_MIN && cL > c && cR > c && (bs < 0 || cL + cR > bsum)) {
+    int bs = -1, dL = 0, nL = 0;
+    double bsum = 0.0, cL = 0.0;
+    const int ns = e - a >= 4 ? e - a - 3 : 0;  // s in [a + 2, e - 2]
+    for (int t = 0; t < 2 * ns; ++t) {
+      const int s = a + 2 + (t >> 1);
+      const bool rt = t & 1;
+      int dd, nn;
+      double cc;
+      eval(rt ? s : a, rt ? e : s, dd, cc, nn);
+      if (!rt) {
+        dL = dd;
+        cL = cc;
+        nL = nn;
+      } else if (nL >= 2 && nn >= 2 && abs(dL - dd) >= SPLIT_MIN && cL > c && cc > c && (bs < 0 || cL + cc > bsum)) {
         bs = s;
-        bsum = cL + cR;
+        bsum = cL + cc;
       }
     }
     return bs;
   };
+  // the ranges to evaluate, depth first and left first (segments come out in piece order): a
+  // range splits at its best split below depth 2 (P.862 utterance_split, two levels), else it is
+  // a segment
   int off[4] = {0, 0, 0, 0}, dl[4] = {0, 0, 0, 0}, n = 0;
-  int D;
-  double c;
-  int nv;
-  eval(0, m, D, c, nv);
-  const int s1 = best_split(0, m, c);
-  if (s1 < 0) {
-    dl[0] = D;
-    n = 1;
-  } else {
-    const int lo[2] = {0, s1}, hi[2] = {s1, m};
-    for (int h = 0; h < 2; ++h) {  // each half once more (depth 2 ends the recursion)
-      int Dh, nh;
-      double ch;
-      eval(lo[h], hi[h], Dh, ch, nh);
-      const int s2 = best_split(lo[h], hi[h], ch);
-      if (s2 < 0) {
-        off[n] = lo[h];
-        dl[n++] = Dh;
-      } else {
-        int Da, Db, na, nb;
-        double ca, cb;
-        eval(lo[h], s2, Da, ca, na);
-        eval(s2, hi[h], Db, cb, nb);
-        off[n] = lo[h];
-        dl[n++] = Da;
-        off[n] = s2;
-        dl[n++] = Db;
-      }
+  int sa[4] = {0, 0, 0, 0}, se[4] = {m, 0, 0, 0}, sdp[4] = {0, 0, 0, 0}, top = 1;
+  while (top > 0) {
+    --top;
+    const int a = sa[top], e = se[top], dep = sdp[top];
+    int D, nv;
+    double c;
+    eval(a, e, D, c, nv);
+    const int sp = dep < 2 ? best_split(a, e, c) : -1;
+    if (sp < 0) {
+      off[n] = a;
+      dl[n++] = D;
+    } else {
+      sa[top] = sp;
+      se[top] = e;
+      sdp[top++] = dep + 1;
+      sa[top] = a;
+      se[top] = sp;
+      sdp[top++] = dep + 1;
     }
   }
   if (tid == 0) {
@@ -851,6 +916,248 @@ __global__ void __launch_bounds__(64) ta_segments_p862(int64_t B, int64_t L, con
   if (nseg) nseg[b] = n;
   if (delay) delay[b] = d;
 }
+
+// ---------------------------------------------------------------- bad intervals (steps 13-15)
+// P.862's realignment of bad intervals (section 10.7 as restated in oracle/align_oracle.py steps
+// 13-15) on the per-frame disturbances of the aligned row (fsem_pesq_distances_f32's frames).
+constexpr float BAD_THR = 30.f;  // THRESHOLD_BAD_FRAMES
+constexpr int BAD_GAP = 4;       // frames: closer bad runs join
+constexpr int BAD_MIN = 5;       // frames: shorter intervals are dropped
+constexpr int MAXBAD = 16;       // intervals per row (include/fsem.h FSEM_PESQ_MAX_BAD)
+constexpr int HOP = 256;         // samples per PESQ frame hop
+
+// PESQ frames of a row (fsem_pesq_frames: PESQ.py:128-133 pads by L % 256, 512-sample frames)
+__host__ __device__ inline int pesq_frames_of(int64_t L) {
+  const int64_t Lp = L + (L % 256);
+  return Lp < 512 ? 0 : (int)(1 + (Lp - 512) / 256);
+}
+
+// One wave per row: the symmetric disturbances 64 frames at a time (a ballot of the bad frames),
+// the runs walked with bit scans in wave-uniform code as ta_utterances; then (lane 0) each
+// interval's samples [256 f0, min(256 f1 + 256, L_row)), the delay of the segment holding its
+// first sample, and its 5120-sample pieces as slot descriptors for ta_fine_partial.
+__global__ void __launch_bounds__(64) ta_bad_find(int64_t B, int64_t L, const int32_t *__restrict__ lengths,
+                                                  const float *__restrict__ frames, int64_t Fcap,
+                                                  const int *__restrict__ nseg, const int *__restrict__ seg_start,
+                                                  const int *__restrict__ seg_delay, int *__restrict__ n_bad,
+                                                  int *__restrict__ bad, int4 *__restrict__ desc,
+                                                  int *__restrict__ ndesc, int *__restrict__ cs_bad, int nslot) {
+  __shared__ int iv[2 * MAXBAD];
+  const int64_t b = blockIdx.x + (int64_t)blockIdx.y * 65535;
+  if (b >= B) return;
+  const int lane = threadIdx.x;
+  const int64_t Lr = row_len(lengths, b, L);
+  const int F = std::min<int64_t>(pesq_frames_of(Lr), Fcap);
+  const float *sym = frames + 2 * b * Fcap;
+  int n = 0, s0 = -1, e0 = -1, rs = -1;  // intervals, joined run [s0, e0), open raw run from rs
+  auto flush = [&]() {
+    if (s0 >= 0 && e0 - s0 >= BAD_MIN && n < MAXBAD) {
+      if (lane == 0) {
+        iv[2 * n] = s0;
+        iv[2 * n + 1] = e0;
+      }
+      ++n;
+    }
+  };
+  auto close_run = [&](int k) {  // the raw run [rs, k) ends
+    if (s0 >= 0 && rs - e0 < BAD_GAP) {
+      e0 = k;
+    } else {
+      flush();
+      s0 = rs;
+      e0 = k;
+    }
+    rs = -1;
+  };
+  for (int k0 = 0; k0 < (F >= 20 ? F : 0); k0 += 64) {
+    const int k = k0 + lane;
+    const uint64_t m = __ballot(k < F && sym[k] > BAD_THR);
+    int pos = 0;
+    while (pos < 64) {
+      if (rs >= 0) {
+        const uint64_t z = ~m >> pos;
+        if (z == 0) break;
+        pos += __builtin_ctzll(z);
+        close_run(k0 + pos);
+      } else {
+        const uint64_t o = m >> pos;
+        if (o == 0) break;
+        pos += __builtin_ctzll(o);
+        rs = k0 + pos;
+      }
+    }
+  }
+  if (rs >= 0) close_run(F);
+  flush();
+  __syncthreads();
+  if (lane == 0) {
+    const int ns = nseg[b];
+    const int *st = seg_start + b * (MAXSEG + 1), *sd = seg_delay + b * MAXSEG;
+    int *o = bad + b * (MAXBAD * 3);
+    int *cb = cs_bad + b * (MAXBAD + 1);
+    int c = 0;
+    for (int i = 0; i < n; ++i) {
+      const int f0 = iv[2 * i], f1 = iv[2 * i + 1];
+      const int a = HOP * f0, e = (int)std::min<int64_t>((int64_t)HOP * f1 + HOP, Lr);
+      int k = 0;
+      while (k + 1 < ns && st[k + 1] <= a) ++k;
+      const int d0 = sd[k];
+      o[3 * i] = f0;
+      o[3 * i + 1] = f1;
+      o[3 * i + 2] = d0;
+      cb[i] = c;
+      for (int p = a; p < e && c < nslot; p += CS) desc[b * nslot + c++] = make_int4(p, std::min(p + CS, e), d0, i);
+    }
+    cb[n] = c;
+    ndesc[b] = c;
+    n_bad[b] = n;
+  }
+}
+
+// Workgroup (interval i, row b): per lag the interval's pieces added in piece order (double), the
+// first maximum above zero, else the segment delay (ta_fine_pick per interval).
+__global__ void __launch_bounds__(256) ta_bad_pick(int64_t B, const int *__restrict__ n_bad,
+                                                   const int *__restrict__ cs_bad, int nslot,
+                                                   const float *__restrict__ part, int *__restrict__ bad) {
+  __shared__ double sv[4];
+  __shared__ int sj[4];
+  const int i = blockIdx.y;  // rows fastest in the dispatch order: a row's active workgroups spread over the XCDs
+  const int64_t b = blockIdx.x + (int64_t)blockIdx.z * 65535;
+  if (b >= B || i >= n_bad[b]) return;
+  const int tid = threadIdx.x;
+  const int c0 = cs_bad[b * (MAXBAD + 1) + i], m = cs_bad[b * (MAXBAD + 1) + i + 1] - c0;
+  const float *P = part + (b * nslot + c0) * (int64_t)(NGRP * LG);
+  double v = 0.0;
+  int j = INT32_MAX;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const int l = tid + 256 * q;
+    if (l >= NLAG) continue;
+    double t = 0.0;
+    for (int s = 0; s < m; ++s) t += P[s * (NGRP * LG) + l];
+    if (t > v) {
+      v = t;
+      j = l;
+    }
+  }
+  block_argmax(v, j, sv, sj);
+  if (tid == 0 && j != INT32_MAX) {
+    int *o = bad + (b * MAXBAD + i) * 3;
+    o[2] = o[2] - FINE + j;
+  }
+}
+
+// The second degraded row: a2[n] = deg[n + D_i] for n in interval i's samples (0 <= n + D_i <
+// L_row), else the aligned row's a[n] (in place allowed: each element is read, then written, by
+// one thread).
+__global__ void __launch_bounds__(256) ta_bad_shift(const float *__restrict__ deg, const float *aligned, int64_t B,
+                                                    int64_t L, int64_t ld, const int32_t *__restrict__ lengths,
+                                                    const int *__restrict__ n_bad, const int *__restrict__ bad,
+                                                    float *out, int64_t ld_out) {
+  __shared__ int lo[MAXBAD], hi[MAXBAD], dl[MAXBAD];
+  const int64_t b = blockIdx.y + (int64_t)blockIdx.z * 65535;
+  if (b >= B) return;
+  const int64_t Lr = row_len(lengths, b, L);
+  const int nb = n_bad[b];
+  if (threadIdx.x < nb) {
+    const int *o = bad + (b * MAXBAD + threadIdx.x) * 3;
+    lo[threadIdx.x] = HOP * o[0];
+    hi[threadIdx.x] = (int)std::min<int64_t>((int64_t)HOP * o[1] + HOP, Lr);
+    dl[threadIdx.x] = o[2];
+  }
+  __syncthreads();
+  const int64_t n = 4 * ((int64_t)blockIdx.x * 256 + threadIdx.x);
+  if (n >= L) return;
+  const float *y = deg + b * ld;
+  float *r = out + b * ld_out;
+  const float *a = aligned + b * ld_out;
+  float v[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    int k = -1;
+    for (int q = 0; q < nb; ++q)
+      if (n + t >= lo[q] && n + t < hi[q]) k = q;
+    if (k < 0) {
+      v[t] = (n + t < L) ? a[n + t] : 0.f;
+    } else {
+      const int64_t m = n + t + dl[k];
+      v[t] = (m >= 0 && m < Lr) ? y[m] : 0.f;
+    }
+  }
+  if (n + 4 <= L) {
+    *reinterpret_cast<float4 *>(r + n) = make_float4(v[0], v[1], v[2], v[3]);
+  } else {
+    for (int t = 0; t < 4 && n + t < L; ++t) r[n + t] = v[t];
+  }
+}
+
+// One wave per row: each interval takes the second row's frames when their symmetric sum is
+// smaller (double, wave order), then PESQ.py:168-172's pooling and :240-243's mapping as
+// pesq_back's pass 3 (windows lane-strided, wave sums in double).
+__global__ void __launch_bounds__(64) ta_bad_pool(const float *__restrict__ frames, const float *__restrict__ frames2,
+                                                  const float *__restrict__ dist, int64_t B, int64_t L,
+                                                  int64_t Fcap, const int32_t *__restrict__ lengths,
+                                                  const int *__restrict__ n_bad, const int *__restrict__ bad,
+                                                  float *__restrict__ mos) {
+  __shared__ int f0s[MAXBAD], f1s[MAXBAD];
+  const int64_t b = blockIdx.x + (int64_t)blockIdx.y * 65535;
+  if (b >= B) return;
+  const int lane = threadIdx.x;
+  const int64_t Lr = row_len(lengths, b, L);
+  const int F = std::min<int64_t>(pesq_frames_of(Lr), Fcap);
+  if (F < 20 || !__builtin_isfinite(dist[b])) {
+    if (lane == 0) mos[b] = __builtin_nanf("");
+    return;
+  }
+  const float *s1 = frames + 2 * b * Fcap, *a1 = s1 + Fcap;
+  const float *s2 = frames2 + 2 * b * Fcap, *a2 = s2 + Fcap;
+  const int nb = n_bad[b];
+  int nu = 0;  // intervals that take the second row's frames (wave-uniform)
+  for (int i = 0; i < nb; ++i) {
+    const int f0 = bad[(b * MAXBAD + i) * 3], f1 = bad[(b * MAXBAD + i) * 3 + 1];
+    double t1 = 0.0, t2 = 0.0;
+    for (int f = f0 + lane; f < f1; f += 64) {
+      t1 += s1[f];
+      t2 += s2[f];
+    }
+    t1 = wave_sum_d(t1);
+    t2 = wave_sum_d(t2);
+    if (t2 < t1) {
+      if (lane == 0) {
+        f0s[nu] = f0;
+        f1s[nu] = f1;
+      }
+      ++nu;
+    }
+  }
+  __syncthreads();
+  const int nw = (F - 20) / 10 + 1;
+  double as_ = 0.0, aa_ = 0.0;
+  for (int w = lane; w < nw; w += 64) {
+    double s6 = 0.0, a6 = 0.0;
+    for (int i = 0; i < 20; ++i) {
+      const int f = 10 * w + i;
+      bool second = false;
+      for (int q = 0; q < nu; ++q) second |= (f >= f0s[q] && f < f1s[q]);
+      const double x = second ? s2[f] : s1[f], y = second ? a2[f] : a1[f];
+      const double x2 = x * x, y2 = y * y;
+      s6 += x2 * x2 * x2;
+      a6 += y2 * y2 * y2;
+    }
+    const double ps = pow(s6 / 20.0, 1.0 / 6.0), pa = pow(a6 / 20.0, 1.0 / 6.0);
+    as_ += ps * ps;
+    aa_ += pa * pa;
+  }
+  as_ = wave_sum_d(as_);
+  aa_ = wave_sum_d(aa_);
+  if (lane == 0) {
+    const double ds = sqrt(as_ / nw), da = sqrt(aa_ / nw);
+    double m = 4.5 - 0.1 * ds - 0.0309 * da;
+    m = 0.999 + 4.0 / (1.0 + exp(-1.3669 * m + 3.8224));
+    mos[b] = (float)m;
+  }
+}
+
 
 inline int64_t frames_cap(int64_t L) { return L / FRAME; }
 inline int64_t nchunks(int64_t L) { return (L + CS - 1) / CS; }
@@ -924,10 +1231,11 @@ inline UttWs utt_carve(void *ws, int64_t B, int64_t L) {
 struct P862Ws {
   float *pv;
   int *pl, *useg;
+  double *pw;
 };
 inline size_t p862_ws_bytes(int64_t B, int64_t L) {
   return utt_ws_bytes(B, L) + 2 * align_up((size_t)(B * nslots(L)) * 4, 256) +
-         align_up((size_t)(B * MAXU * USEG_P) * 4, 256);
+         align_up((size_t)(B * MAXU * USEG_P) * 4, 256) + align_up((size_t)(B * nslots(L)) * 8, 256);
 }
 inline P862Ws p862_carve(void *ws, int64_t B, int64_t L) {
   char *p = static_cast<char *>(ws) + utt_ws_bytes(B, L);
@@ -937,6 +1245,33 @@ inline P862Ws p862_carve(void *ws, int64_t B, int64_t L) {
   w.pl = reinterpret_cast<int *>(p);
   p += align_up((size_t)(B * nslots(L)) * 4, 256);
   w.useg = reinterpret_cast<int *>(p);
+  p += align_up((size_t)(B * MAXU * USEG_P) * 4, 256);
+  w.pw = reinterpret_cast<double *>(p);
+  return w;
+}
+
+// bad-interval workspace: the slot descriptors (an interval's pieces: at most nchunks + MAXBAD per
+// row, the intervals being disjoint), their counts, the intervals' first slots, the partials
+inline int64_t bad_nslots(int64_t L) { return nchunks(L) + MAXBAD; }
+struct BadWs {
+  int4 *desc;
+  int *ndesc, *cs;
+  float *part;
+};
+inline size_t bad_ws_bytes(int64_t B, int64_t L) {
+  return align_up((size_t)(B * bad_nslots(L)) * sizeof(int4), 256) + align_up((size_t)B * 4, 256) +
+         align_up((size_t)(B * (MAXBAD + 1)) * 4, 256) + align_up((size_t)(B * bad_nslots(L) * NGRP * LG) * 4, 256);
+}
+inline BadWs bad_carve(void *ws, int64_t B, int64_t L) {
+  char *p = static_cast<char *>(ws);
+  BadWs w;
+  w.desc = reinterpret_cast<int4 *>(p);
+  p += align_up((size_t)(B * bad_nslots(L)) * sizeof(int4), 256);
+  w.ndesc = reinterpret_cast<int *>(p);
+  p += align_up((size_t)B * 4, 256);
+  w.cs = reinterpret_cast<int *>(p);
+  p += align_up((size_t)(B * (MAXBAD + 1)) * 4, 256);
+  w.part = reinterpret_cast<float *>(p);
   return w;
 }
 
@@ -1037,8 +1372,7 @@ static int time_align_segmented(bool p862, const float *ref, const float *deg, i
   align::ta_utterances<<<xy(batch), 64, 0, st>>>(batch, length, lengths, w.E, nfr_cap, w.nutt, w.utt, w.reg, w.cs);
   FSEM_CHECK_LAUNCH();
   {
-    dim3 grid = yz(batch);
-    grid.x = align::MAXU;
+    const dim3 grid((unsigned)std::min<int64_t>(batch, 65535), align::MAXU, (unsigned)((batch + 65534) / 65535));
     align::ta_crude_utt<<<grid, 256, 0, st>>>(batch, length, lengths, w.E, nfr_cap, max_frames, w.crude, w.nutt,
                                               w.utt, w.ucrude);
     FSEM_CHECK_LAUNCH();
@@ -1048,18 +1382,16 @@ static int time_align_segmented(bool p862, const float *ref, const float *deg, i
   FSEM_CHECK_LAUNCH();
   if (p862) {
     const align::P862Ws q = align::p862_carve(ws, batch, length);
-    align::ta_piece_peaks<<<(unsigned)((batch * nsl + 3) / 4), 256, 0, st>>>(batch * nsl, w.part, q.pv, q.pl);
+    align::ta_piece_peaks<<<(unsigned)((batch * nsl + 3) / 4), 256, 0, st>>>(batch * nsl, w.part, q.pv, q.pl, q.pw);
     FSEM_CHECK_LAUNCH();
-    dim3 grid = yz(batch);
-    grid.x = align::MAXU;
-    align::ta_pick_p862<<<grid, 256, 0, st>>>(batch, w.nutt, w.cs, w.ucrude, (int)nsl, q.pv, q.pl, q.useg);
+    const dim3 grid((unsigned)std::min<int64_t>(batch, 65535), align::MAXU, (unsigned)((batch + 65534) / 65535));
+    align::ta_pick_p862<<<grid, 256, 0, st>>>(batch, w.nutt, w.cs, w.ucrude, (int)nsl, q.pv, q.pl, q.pw, q.useg);
     FSEM_CHECK_LAUNCH();
     align::ta_segments_p862<<<(unsigned)((batch + 63) / 64), 64, 0, st>>>(batch, length, lengths, w.nutt, w.reg,
                                                                           q.useg, ns, ss, sd, dl);
     FSEM_CHECK_LAUNCH();
   } else {
-    dim3 grid = yz(batch);
-    grid.x = align::MAXU;
+    const dim3 grid((unsigned)std::min<int64_t>(batch, 65535), align::MAXU, (unsigned)((batch + 65534) / 65535));
     align::ta_pick_utt<<<grid, 256, 0, st>>>(batch, w.nutt, w.cs, w.ucrude, (int)nsl, w.part, w.useg);
     FSEM_CHECK_LAUNCH();
     align::ta_segments<<<(unsigned)((batch + 63) / 64), 64, 0, st>>>(batch, length, lengths, w.nutt, w.reg, w.useg,
@@ -1096,4 +1428,65 @@ extern "C" int fsem_time_align_p862_f32(const float *ref, const float *deg, int6
                                         void *stream) {
   return time_align_segmented(true, ref, deg, batch, length, ld, lengths, max_delay, delay, n_seg, seg_start,
                               seg_delay, deg_aligned, ld_out, ws, ws_bytes, stream);
+}
+
+extern "C" size_t fsem_pesq_bad_intervals_workspace_bytes(int64_t batch, int64_t length) {
+  if (batch <= 0 || length <= 0) return 0;
+  return align::bad_ws_bytes(batch, length);
+}
+
+extern "C" int fsem_pesq_bad_intervals_f32(const float *ref, const float *deg, const float *deg_aligned,
+                                           int64_t batch, int64_t length, int64_t ld, const int32_t *lengths,
+                                           const float *frames, const int32_t *n_seg, const int32_t *seg_start,
+                                           const int32_t *seg_delay, int32_t *n_bad, int32_t *bad,
+                                           float *deg_second, int64_t ld_out, void *ws, size_t ws_bytes,
+                                           void *stream) {
+  if (!ref || !deg || !deg_aligned || !frames || !n_seg || !seg_start || !seg_delay || !n_bad || !bad ||
+      !deg_second || batch <= 0 || length <= 0 || ld < length || length > kMaxLength || ld_out < length ||
+      ld_out % 4 != 0 || ld % 4 != 0)
+    return FSEM_EINVAL;
+  const int64_t nsl = align::bad_nslots(length);
+  if (batch * nsl > INT32_MAX) return FSEM_EINVAL;
+  if (!ws || ws_bytes < align::bad_ws_bytes(batch, length)) return FSEM_EWORKSPACE;
+  hipStream_t st = (hipStream_t)stream;
+  const align::BadWs w = align::bad_carve(ws, batch, length);
+  const int64_t Fcap = align::pesq_frames_of(length);
+  auto yz = [](int64_t n) { return dim3(1, (unsigned)std::min<int64_t>(n, 65535), (unsigned)((n + 65534) / 65535)); };
+  auto xy = [](int64_t n) { return dim3((unsigned)std::min<int64_t>(n, 65535), (unsigned)((n + 65534) / 65535)); };
+  align::ta_bad_find<<<xy(batch), 64, 0, st>>>(batch, length, lengths, frames, Fcap, n_seg, seg_start, seg_delay,
+                                               n_bad, bad, w.desc, w.ndesc, w.cs, (int)nsl);
+  FSEM_CHECK_LAUNCH();
+  align::UttTables ut{};
+  ut.desc = w.desc;
+  ut.ndesc = w.ndesc;
+  align::ta_fine_partial<<<(unsigned)(batch * nsl), 256, 0, st>>>(ref, deg, batch, length, ld, lengths, nullptr,
+                                                                  (int)nsl, w.part, ut);
+  FSEM_CHECK_LAUNCH();
+  {
+    const dim3 grid((unsigned)std::min<int64_t>(batch, 65535), align::MAXBAD, (unsigned)((batch + 65534) / 65535));
+    align::ta_bad_pick<<<grid, 256, 0, st>>>(batch, n_bad, w.cs, (int)nsl, w.part, bad);
+    FSEM_CHECK_LAUNCH();
+  }
+  {
+    dim3 grid = yz(batch);
+    grid.x = (unsigned)((length + 1023) / 1024);
+    align::ta_bad_shift<<<grid, 256, 0, st>>>(deg, deg_aligned, batch, length, ld, lengths, n_bad, bad, deg_second,
+                                              ld_out);
+    FSEM_CHECK_LAUNCH();
+  }
+  return FSEM_OK;
+}
+
+extern "C" int fsem_pesq_pool_f32(const float *frames, const float *frames2, const float *dist, int64_t batch,
+                                  int64_t length, const int32_t *lengths, const int32_t *n_bad, const int32_t *bad,
+                                  float *mos, void *stream) {
+  if (!frames || !frames2 || !dist || !n_bad || !bad || !mos || batch <= 0 || length <= 0 || length > kMaxLength)
+    return FSEM_EINVAL;
+  const int64_t Fcap = align::pesq_frames_of(length);
+  if (Fcap < 20 && !lengths) return FSEM_ESHORT;
+  auto xy = [](int64_t n) { return dim3((unsigned)std::min<int64_t>(n, 65535), (unsigned)((n + 65534) / 65535)); };
+  align::ta_bad_pool<<<xy(batch), 64, 0, (hipStream_t)stream>>>(frames, frames2, dist, batch, length, Fcap, lengths,
+                                                                 n_bad, bad, mos);
+  FSEM_CHECK_LAUNCH();
+  return FSEM_OK;
 }

@@ -63,7 +63,7 @@ extern "C" {
 #define FSEM_ERATE -5         /* unsupported sample-rate pair (see resampling)      */
 
 const char *fsem_strerror(int code);
-int fsem_version(void);  /* 8: + fsem_time_align_p862_*; 7: + fsem_host_buffer_mapped; 6: + fsem_build_id; 5: + fsem_time_align_utt_*; 4: + fsem_pre_emphasize_f32; 3: time alignment, distances */
+int fsem_version(void);  /* 9: + fsem_pesq_bad_intervals_*, fsem_pesq_pool_f32; 8: + fsem_time_align_p862_*; 7: + fsem_host_buffer_mapped; 6: + fsem_build_id; 5: + fsem_time_align_utt_*; 4: + fsem_pre_emphasize_f32; 3: time alignment, distances */
 /* Content hash (16 hex digits) of the sources, headers and compile flags this library was built
  * from (fast_speech_enhancement_metrics_amd/_build.py source_hash); the host layer refuses a
  * library whose id differs from its own tree's.  "unknown" for builds outside _build.py. */
@@ -271,6 +271,39 @@ int fsem_time_align_p862_f32(const float *ref, const float *deg, int64_t batch, 
                              int32_t *n_seg, int32_t *seg_start, int32_t *seg_delay,
                              float *deg_aligned, int64_t ld_out, void *ws, size_t ws_bytes,
                              void *stream);
+
+/* bad intervals (ABI 9): P.862's realignment of bad intervals after the perceptual model (section
+ * 10.7, restated in oracle/align_oracle.py steps 13-15; parity against P.862 implementations
+ * unpinned), for the P.862 mode's rows.  Replaces nothing in the reference.
+ *   deg_aligned : [batch, length] float32 (row stride ld_out): fsem_time_align_p862_f32's output
+ *   frames      : [batch, 2, Fcap] float32 (Fcap = fsem_pesq_frames(length)):
+ *                 fsem_pesq_distances_f32's per-frame disturbances of (ref, deg_aligned)
+ *   n_seg, seg_start, seg_delay : that alignment's segments
+ *   n_bad       : [batch] int32 output: intervals per row (0 .. FSEM_PESQ_MAX_BAD)
+ *   bad         : [batch, FSEM_PESQ_MAX_BAD, 3] int32 output: {first frame, end frame, delay} --
+ *                 runs of frames with symmetric disturbance > 30, joined across gaps < 4 frames,
+ *                 from 5 frames long, in order; delay: the first maximum of the first-difference
+ *                 correlation over the interval's samples [256 f0, min(256 f1 + 256, lengths[b]))
+ *                 within +-383 of the delay of the segment holding its first sample (that delay
+ *                 when no lag correlates positively)
+ *   deg_second  : [batch, length] float32 output (row stride ld_out; may be deg_aligned itself):
+ *                 deg[b][n + delay_i] for n in interval i (0 <= n + delay_i < lengths[b], else 0),
+ *                 deg_aligned[b][n] elsewhere
+ * pool: the MOS of each row from the first frames, an interval taking frames2 (the per-frame
+ *   disturbances of (ref, deg_second)) when their symmetric sum over it is smaller; the pooling
+ *   and mapping of fsem_pesq_wb_f32 (PESQ.py:168-172, 240-243).  dist: [2, batch] the first
+ *   distances (NaN there gives NaN); rows under 20 frames give NaN.
+ */
+#define FSEM_PESQ_MAX_BAD 16
+size_t fsem_pesq_bad_intervals_workspace_bytes(int64_t batch, int64_t length);
+int fsem_pesq_bad_intervals_f32(const float *ref, const float *deg, const float *deg_aligned, int64_t batch,
+                                int64_t length, int64_t ld, const int32_t *lengths, const float *frames,
+                                const int32_t *n_seg, const int32_t *seg_start, const int32_t *seg_delay,
+                                int32_t *n_bad, int32_t *bad, float *deg_second, int64_t ld_out, void *ws,
+                                size_t ws_bytes, void *stream);
+int fsem_pesq_pool_f32(const float *frames, const float *frames2, const float *dist, int64_t batch,
+                       int64_t length, const int32_t *lengths, const int32_t *n_bad, const int32_t *bad,
+                       float *mos, void *stream);
 
 #ifdef __cplusplus
 }

@@ -435,3 +435,101 @@ def align_p862(ref: np.ndarray, deg: np.ndarray, max_delay: int = 16000, lengths
         out[b, :n] = shift_segments(deg[b, :n], st, dl)
         segs.append((st, dl))
     return out, ds, segs
+
+
+# ----------------------------------------------------------------------------- bad intervals
+# P.862 realigns "bad intervals" after its perceptual model (section 10.7, restated): with the
+# segment-aligned degraded row scored,
+# 13. bad frames are those whose symmetric frame disturbance exceeds BAD_THR (P.862's
+#     THRESHOLD_BAD_FRAMES); runs of them closer than BAD_GAP frames join, intervals from BAD_MIN
+#     frames are kept (at most MAXBAD per row, in order);
+# 14. each interval's samples [256 f0, 256 f1 + 256) get the first-difference correlation's first
+#     maximum within +-FINE of the delay of the segment holding sample 256 f0 (that delay if no lag
+#     correlates positively), and a second degraded row takes those samples at that delay;
+# 15. the second row is scored too, and an interval's frames take its symmetric and asymmetric
+#     disturbances when their symmetric sum over the interval is smaller (P.862 keeps the better
+#     alignment of a bad interval); the MOS pools the combined frames as PESQ.py:168-172, 240-243.
+BAD_THR = 30.0
+BAD_GAP = 4
+BAD_MIN = 5
+MAXBAD = 16
+HOP = 256
+
+
+def bad_intervals(sym: np.ndarray) -> list:
+    """Step 13: [(f0, f1)] frames of one row's bad intervals."""
+    bad = np.asarray(sym) > BAD_THR
+    runs, f, n = [], 0, bad.shape[0]
+    while f < n:
+        if bad[f]:
+            e = f
+            while e < n and bad[e]:
+                e += 1
+            if runs and f - runs[-1][1] < BAD_GAP:
+                runs[-1][1] = e
+            else:
+                runs.append([f, e])
+            f = e
+        else:
+            f += 1
+    return [(a, b) for a, b in runs if b - a >= BAD_MIN][:MAXBAD]
+
+
+def interval_delay(ref: np.ndarray, deg: np.ndarray, a: int, b: int, d0: int) -> int:
+    """Step 14: the interval's delay over samples [a, b) within +-FINE of d0."""
+    r = np.asarray(ref, dtype=np.float64)
+    d = np.asarray(deg, dtype=np.float64)
+    L = r.shape[0]
+    wr = np.zeros(L)
+    wd = np.zeros(L)
+    wr[1:] = np.diff(r)
+    wd[1:] = np.diff(d)
+    best, arg = 0.0, d0
+    for D in range(d0 - FINE, d0 + FINE + 1):
+        lo, hi = max(a, 1, 1 - D), min(b, L, L - D)
+        if hi <= lo:
+            continue
+        c = float(np.dot(wr[lo:hi], wd[lo + D:hi + D]))
+        if c > best:
+            best, arg = c, D
+    return arg
+
+
+def realign_bad(ref, deg, aligned, seg_start, seg_delay, sym):
+    """Step 14 for one row: ([(f0, f1, delay)], the second degraded row)."""
+    L = deg.shape[0]
+    out = np.array(aligned, copy=True)
+    res = []
+    for f0, f1 in bad_intervals(sym):
+        a, b = HOP * f0, min(HOP * f1 + HOP, L)
+        k = int(np.searchsorted(seg_start, a, side="right")) - 1
+        D = interval_delay(ref, deg, a, b, int(seg_delay[k]))
+        res.append((f0, f1, D))
+        for n in range(a, b):
+            out[n] = deg[n + D] if 0 <= n + D < L else 0.0
+    return res, out
+
+
+def pesq_p862(ref: np.ndarray, deg: np.ndarray, max_delay: int = 16000):
+    """(MOS [B], [[(f0, f1, delay)] per row]) of [B, L] rows: P.862-mode alignment, then the
+    bad-interval realignment (steps 13-15) on the oracle's PESQ model."""
+    from oracle import pesq_oracle as po
+    ref = np.atleast_2d(ref).astype(np.float32)
+    deg = np.atleast_2d(deg).astype(np.float32)
+    aligned, _, segs = align_p862(ref, deg, max_delay)
+    i1, i2 = {}, {}
+    po.disturbances(ref, aligned, i1)
+    s1, a1 = i1["sym_frame"].copy(), i1["asym_frame"].copy()
+    second = np.array(aligned, copy=True)
+    bad = []
+    for b in range(ref.shape[0]):
+        res, second[b] = realign_bad(ref[b], deg[b], aligned[b], segs[b][0], segs[b][1], s1[b])
+        bad.append(res)
+    po.disturbances(ref, second, i2)
+    s2, a2 = i2["sym_frame"], i2["asym_frame"]
+    for b, res in enumerate(bad):
+        for f0, f1, _ in res:
+            if s2[b, f0:f1].sum() < s1[b, f0:f1].sum():
+                s1[b, f0:f1] = s2[b, f0:f1]
+                a1[b, f0:f1] = a2[b, f0:f1]
+    return po.mos_from_distances(po.overlapping_sums(s1), po.overlapping_sums(a1)), bad

@@ -81,3 +81,44 @@ def continuous_pair(seed: int, L: int, pieces):
 # one utterance, three delays: two levels of the P.862 mode's split
 L_CONT = 128000
 CONT_PIECES = [(0, 40000, 100), (40000, 85000, 400), (85000, L_CONT, -200)]
+
+
+def gated_pair(seed: int, L: int, jumps, D0: int = 150):
+    """(clean, degraded) float32 rows of one continuous utterance of 7 Hz gated coloured noise
+    (bursts of about 90 ms: a frame misaligned by a few hundred samples scores far worse than an
+    aligned one) delayed by D0, except the short stretches jumps = [(start, end, D)] -- too short
+    for the alignment's 320 ms pieces to split on, so they remain as bad intervals of the
+    segment-aligned row for the P.862 realignment (oracle/align_oracle.py steps 13-15)."""
+    rng = np.random.default_rng(seed)
+    t = np.arange(L) / 16000
+    x = np.convolve(rng.standard_normal(L + 64), np.hanning(9), "same")[:L]
+    gate = (np.sin(2 * np.pi * 7 * t + seed) > 0.3).astype(np.float64)
+    gate = np.convolve(gate, np.hanning(65) / np.hanning(65).sum(), "same")
+    c = x * (0.05 + gate)
+    n = c + 0.03 * rng.standard_normal(L)
+    deg = 1e-3 * rng.standard_normal(L)
+    pieces, p = [], 0
+    for a, b, D in jumps:
+        pieces += [(p, a, D0), (a, b, D)]
+        p = b
+    pieces.append((p, L, D0))
+    for a, b, D in pieces:
+        seg = np.zeros(L)
+        seg[a:b] = n[a:b]
+        deg += _shift(seg, D)
+    return c.astype(np.float32), deg.astype(np.float32)
+
+
+# rows with delay jumps of 150-250 ms: (seed, jumps, the intervals' delays the realignment finds)
+BAD_CASES = [
+    (11, [(20000, 23000, 450)], None),
+    (12, [(30000, 32600, -100), (60000, 63000, 420)], [-100, 420]),
+    (13, [], []),
+    (14, [(50000, 54000, -200)], [-200]),
+]
+
+
+def bad_batch():
+    """[B, L_UTT] clean / degraded rows of BAD_CASES."""
+    rows = [gated_pair(s, L_UTT, j) for s, j, _ in BAD_CASES]
+    return np.stack([r[0] for r in rows]), np.stack([r[1] for r in rows])

@@ -92,6 +92,6 @@ def test_pesq_time_align_utterance_mode(utt_batch):
     np.testing.assert_array_equal(got.numpy(), want.numpy())
     np.testing.assert_array_equal(m.last_delays.numpy(), ds)
     with pytest.raises(ValueError):
-        PESQ(16000, time_align="p862")
+        PESQ(16000, time_align="frames")
     with pytest.raises(ValueError):
         time_align(torch.from_numpy(c), torch.from_numpy(d), mode="frames")
