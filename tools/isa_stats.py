@@ -39,19 +39,41 @@ def stats(body):
     }
 
 
+def resources(text):
+    """name -> the compiler's resource metadata (amdhsa.kernels: registers, spills, LDS, scratch)."""
+    out = {}
+    i = text.find("amdhsa.kernels:")
+    if i < 0:
+        return out
+    for entry in re.split(r"\n  - ", text[i:]):
+        m = re.search(r"^\s+\.name:\s+(\S+)", entry, re.M)
+        if not m:
+            continue
+        r = {}
+        for key in ("vgpr_count", "agpr_count", "sgpr_count", "vgpr_spill_count", "sgpr_spill_count",
+                    "group_segment_fixed_size", "private_segment_fixed_size"):
+            k = re.search(r"\." + key + r":\s+(\d+)", entry)
+            if k:
+                r[key] = int(k.group(1))
+        out[m.group(1)] = r
+    return out
+
+
 def main():
     text = open(sys.argv[1]).read()
     filt = sys.argv[2] if len(sys.argv) > 2 else ""
-    meta = {}
-    for m in re.finditer(r"\.name:\s+(\w+)\n(.*?)(?=\n  - \.|\Z)", text, re.S):
-        pass
+    res = resources(text)
+    short = {"vgpr_count": "vgpr", "agpr_count": "agpr", "sgpr_count": "sgpr", "vgpr_spill_count": "vgpr_spill",
+             "sgpr_spill_count": "sgpr_spill", "group_segment_fixed_size": "lds_bytes",
+             "private_segment_fixed_size": "scratch_bytes"}
     for name, body in kernels(text):
         if filt not in name:
             continue
         s = stats(body)
-        ms = re.search(r"\.sgpr_spill_count:\s+(\d+)[^\n]*\n(?:.*\n){0,40}?.*\.symbol:\s+" + re.escape(name), text)
         print(name[:90])
         print("   " + "  ".join(f"{k} {v}" for k, v in s.items()))
+        if name in res:
+            print("   " + "  ".join(f"{short[k]} {v}" for k, v in res[name].items()))
 
 
 if __name__ == "__main__":
