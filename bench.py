@@ -68,7 +68,7 @@ def parse():
                          "multidevice.py) on a batch of N x --batch rows held by device 0 -- the timed "
                          "call includes the peer copies of the other devices' shards over xGMI")
     ap.add_argument("--workload", default="c2",
-                    choices=["c2", "pesq", "pesq_aligned", "pesq_aligned_utt", "c3", "c5"],
+                    choices=["c2", "pesq", "pesq_aligned", "pesq_aligned_utt", "pesq_aligned_p862", "c3", "c5"],
                     help="c2: BASELINE metric (default, PESQ-wb + STOI/ESTOI); pesq: configs[1] as stated, "
                          "PESQ-wb only; c3: STOI+ESTOI only, 8192 x 5 s @ 16 kHz per GPU; "
                          "c5: config 5, mixed 8/16 kHz ragged 2-30 s batch")
@@ -370,8 +370,8 @@ def run_pesq(args, world, rank, dev, distributed):
     from fast_speech_enhancement_metrics_amd.synthetic import speech_like_pairs
     B, L = 4096, 160000
     clean, noisy, _ = speech_like_pairs(B, L, 16000, seed=42 + rank, device=dev)
-    aligned = args.workload in ("pesq_aligned", "pesq_aligned_utt")
-    mode = "utterance" if args.workload == "pesq_aligned_utt" else "row"
+    aligned = args.workload in ("pesq_aligned", "pesq_aligned_utt", "pesq_aligned_p862")
+    mode = {"pesq_aligned_utt": "utterance", "pesq_aligned_p862": "p862"}.get(args.workload, "row")
     if aligned:
         # extension (not in the reference): degraded rows delayed by U[-2000, 2000] samples,
         # PESQ(time_align=True) estimates and undoes the delay before scoring (alignment.py)
@@ -552,8 +552,9 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    if args.workload in ("pesq", "pesq_aligned", "pesq_aligned_utt", "c3", "c5"):
-        {"pesq": run_pesq, "pesq_aligned": run_pesq, "pesq_aligned_utt": run_pesq, "c3": run_c3,
+    if args.workload in ("pesq", "pesq_aligned", "pesq_aligned_utt", "pesq_aligned_p862", "c3", "c5"):
+        {"pesq": run_pesq, "pesq_aligned": run_pesq, "pesq_aligned_utt": run_pesq, "pesq_aligned_p862": run_pesq,
+         "c3": run_c3,
          "c5": run_c5}[args.workload](
             args, world, rank, dev, distributed)
         if distributed:
