@@ -158,6 +158,66 @@ __device__ __forceinline__ void fft512_wave(cf vc[8], float2 *buf, int lane, con
 }
 
 
+// Two 512-point FFTs of one wave through ONE exchange area, software-pipelined: each FFT's
+// butterflies run while the other's exchange is in flight (one LDS round trip per exchange
+// instead of two back-to-back FFTs' four each).  A wave's LDS operations execute in issue
+// order, so a gather issued before the other FFT's scatter reads its data first (write after
+// read within the wave); the fences wait for scatters before the gathers that read them.
+// Results as two fft512_wave calls (the same operations per element, in the same order).
+__device__ __forceinline__ void fft512_wave_x2(cf va[8], cf vb[8], float2 *buf, int lane, const cf tw1[8],
+                                               const cf tw2[8]) {
+  f2 a[8], b[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    a[r] = (f2){va[r].r, va[r].i};
+    b[r] = (f2){vb[r].r, vb[r].i};
+  }
+  const int o1 = (lane >> 3) * 64 + (lane & 7);
+  auto scatter1 = [&](const f2 *v) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) buf[fpad(8 * lane + r)] = make_float2(v[r].x, v[r].y);
+  };
+  auto scatter2 = [&](const f2 *v) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) buf[fpad(o1 + 8 * r)] = make_float2(v[r].x, v[r].y);
+  };
+  auto gather = [&](f2 *v) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const float2 t = buf[fpad(lane + 64 * r)];
+      v[r] = (f2){t.x, t.y};
+    }
+  };
+  dft8v(a);
+  scatter1(a);
+  dft8v(b);  // beside A's first scatter
+  wave_lds_fence();
+  gather(a);
+  scatter1(b);  // after A's gather in issue order
+  twiddle7(a, tw1);
+  dft8v(a);  // beside B's first scatter
+  wave_lds_fence();
+  gather(b);
+  scatter2(a);
+  twiddle7(b, tw1);
+  dft8v(b);  // beside A's second scatter
+  wave_lds_fence();
+  gather(a);
+  scatter2(b);
+  twiddle7(a, tw2);
+  dft8v(a);  // beside B's second scatter
+  wave_lds_fence();
+  gather(b);
+  twiddle7(b, tw2);
+  dft8v(b);
+  wave_lds_fence();
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    va[r] = {a[r].x, a[r].y};
+    vb[r] = {b[r].x, b[r].y};
+  }
+}
+
 // Per-lane twiddles of stages 1 and 2: W512^(8 r (lane&7)) and W512^(r lane).
 __device__ __forceinline__ void fft512_twiddles(int lane, cf tw1[8], cf tw2[8]) {
 #pragma unroll

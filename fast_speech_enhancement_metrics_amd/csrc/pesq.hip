@@ -915,76 +915,86 @@ __global__ void __launch_bounds__(PT, 2)
     const int nfr = min(NF, rg.F - g * NF);  // valid frames in this segment
     float2 *wbuf = reinterpret_cast<float2 *>(xbuf) + wave * kFftBuf;
     const int nrounds = nfr > 0 ? (nfr + 7) / 8 : 0;
-    // RPB rounds per barrier: their spectra are held (8 RPB values per lane) until every wave
-    // has read the tile for them, then parked; the parking of rounds rd .. rd+RPB-1 stays below
-    // the inputs of round rd+RPB (258 (8 rd + 8 RPB) <= 768 + 2048 (rd + RPB))
-    constexpr int RPB = 3;
-    static_assert(SPEC_LD * 8 * RPB <= WARM + 256 * 8 * RPB && SPEC_LD * NF <= WARM + 256 * NF,
-                  "parking below the next rounds' inputs");
     // the 12 distinct tile samples of a frame pair (frame a: [0, 512), frame b: [256, 768))
     auto load_pair = [&](int fa, float o[12]) {
       const float *fra = tile + WARM + 256 * fa;  // in the tile for every fa < 2 (4 * 6)
 #pragma unroll
       for (int r = 0; r < 12; ++r) o[r] = fra[lane + 64 * r];
     };
-    static_assert(WARM + 256 * (2 * (4 * (RPB * ((NF / 8 + RPB - 1) / RPB) - 1) + 3)) + 768 <= TILE + TILE_PAD,
-                  "frame-pair reads of every round stay in the tile");
-    for (int rd = 0; rd < nrounds; rd += RPB) {
-      float pa[RPB][4], pb[RPB][4];
-      float cur[12];
-      load_pair(2 * (4 * rd + wave), cur);
+    auto power_split = [&](const cf v[8], float *qa, float *qb) {
 #pragma unroll
-      for (int h = 0; h < RPB; ++h) {
-        const int fa = 2 * (4 * (rd + h) + wave);
-        // the next pair's samples are read before this pair's FFT, their LDS latency hidden
-        // behind its butterflies (measured 2.534 -> 2.521 ms per 2048-row launch; reading the
-        // next barrier group's first pair too spills VGPRs: 2.572)
-        float nxt[12];
-        if (h + 1 < RPB) load_pair(2 * (4 * (rd + h + 1) + wave), nxt);
-        if (fa < nfr) {
-          cf v[8];
-#pragma unroll
-          for (int r = 0; r < 8; ++r) {  // one v_pk_mul_f32 per pair (the window broadcast)
-            typedef float f2v __attribute__((ext_vector_type(2)));
-            const f2v w2 = (f2v){cur[r], cur[r + 4]} * (f2v){win[r], win[r]};
-            v[r] = {w2.x, w2.y};
-          }
-          fft512_wave(v, wbuf, lane, tw1, tw2);
-          if (FSEM_DOUBLE == 4) fft512_wave(v, wbuf, lane, tw1, tw2);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float mr = __shfl(v[7 - r].r, plane, 64);
-            float mi = __shfl(v[7 - r].i, plane, 64);
-            if (lane == 0) {
-              mr = v[(8 - r) & 7].r;
-              mi = v[(8 - r) & 7].i;
-            }
-            // 4 |Z_a|^2, 4 |Z_b|^2 (the 1/4 is folded into the Bark weights, bcor) in packed FP32:
-            // (|zr + mr|^2 + (zi - mi)^2, |zi + mi|^2 + (zr - mr)^2), the scalar form's operations
-            typedef float f2v __attribute__((ext_vector_type(2)));
-            const f2v z = {v[r].r, v[r].i}, m = {mr, mi};
-            const f2v sm = z + m;
-            const f2v df = z.yx - m.yx;
-            const f2v pp = __builtin_elementwise_fma(sm, sm, df * df);
-            pa[h][r] = pp.x;
-            pb[h][r] = pp.y;
-          }
-          if (lane == 0) {  // spec[:, :, 0] = 0 (PESQ.py:136)
-            pa[h][0] = 0.f;
-            pb[h][0] = 0.f;
-          }
+      for (int r = 0; r < 4; ++r) {
+        float mr = __shfl(v[7 - r].r, plane, 64);
+        float mi = __shfl(v[7 - r].i, plane, 64);
+        if (lane == 0) {
+          mr = v[(8 - r) & 7].r;
+          mi = v[(8 - r) & 7].i;
         }
-        if (h + 1 < RPB) {
+        typedef float f2v __attribute__((ext_vector_type(2)));
+        const f2v z = {v[r].r, v[r].i}, m = {mr, mi};
+        const f2v sm = z + m;
+        const f2v df = z.yx - m.yx;
+        const f2v pp = __builtin_elementwise_fma(sm, sm, df * df);
+        qa[r] = pp.x;
+        qb[r] = pp.y;
+      }
+      if (lane == 0) {
+        qa[0] = 0.f;
+        qb[0] = 0.f;
+      }
+    };
+    auto window = [&](const float c[12], cf v[8]) {
 #pragma unroll
-          for (int r = 0; r < 12; ++r) cur[r] = nxt[r];
+      for (int r = 0; r < 8; ++r) {
+        typedef float f2v __attribute__((ext_vector_type(2)));
+        const f2v w2 = (f2v){c[r], c[r + 4]} * (f2v){win[r], win[r]};
+        v[r] = {w2.x, w2.y};
+      }
+    };
+    // Rounds of 8 frames (one frame pair per wave) in chunks of two rounds: each wave transforms
+    // its two pairs of a chunk together (fft512_wave_x2: one pair's butterflies beside the other's
+    // LDS exchange, one exchange area), GR = 2 chunks per barrier.  Their spectra are held (16
+    // values per lane) until every wave has read the tile for them, then parked in the consumed
+    // part of the tile, below the next chunks' inputs.  (Round 6: the front end 4.389 -> 4.329 ms
+    // against one pair at a time with the next pair's samples read ahead; reading the next chunk
+    // ahead here spills VGPRs and loses 1.5 %, profiles/r6_g/.)
+    constexpr int GR = 2;
+    static_assert(SPEC_LD * 8 * 2 * GR <= WARM + 256 * 8 * 2 * GR, "parking below the next rounds' inputs");
+    const int nchunk = (nrounds + 1) / 2;
+    // chunks k < nchunk <= 3 read rounds <= 5, inside the tile (as the RPB = 3 plan's reads)
+    static_assert(WARM + 256 * (2 * (4 * 5 + 3)) + 768 <= TILE + TILE_PAD && NF / 8 <= 6, "chunk reads in the tile");
+    auto load_chunk = [&](int k, float (*c)[12]) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) load_pair(2 * (4 * (2 * k + h) + wave), c[h]);
+    };
+    for (int k0 = 0; k0 < nchunk; k0 += GR) {
+      float pa[2 * GR][4], pb[2 * GR][4];
+#pragma unroll
+      for (int q = 0; q < GR; ++q) {
+        const int k = k0 + q;
+        if (k >= nchunk) break;  // wave-uniform
+        const int f0 = 2 * (4 * (2 * k) + wave), f1 = 2 * (4 * (2 * k + 1) + wave);
+        float cc[2][12];
+        load_chunk(k, cc);
+        cf v0[8], v1[8];
+        window(cc[0], v0);
+        window(cc[1], v1);
+        if (f1 < nfr) {
+          fft512_wave_x2(v0, v1, wbuf, lane, tw1, tw2);
+          if (FSEM_DOUBLE == 4) fft512_wave_x2(v0, v1, wbuf, lane, tw1, tw2);
+          power_split(v0, pa[2 * q], pb[2 * q]);
+          power_split(v1, pa[2 * q + 1], pb[2 * q + 1]);
+        } else if (f0 < nfr) {
+          fft512_wave(v0, wbuf, lane, tw1, tw2);
+          power_split(v0, pa[2 * q], pb[2 * q]);
         }
       }
       lds_barrier();  // every wave is done reading the tile for these rounds
-      STAMP(6 + rd);
+      STAMP(6 + k0);
 #pragma unroll
-      for (int h = 0; h < RPB; ++h) {
-        const int fa = 2 * (4 * (rd + h) + wave);
-        if (fa < nfr) {  // park the spectra in the consumed part of the tile
+      for (int h = 0; h < 2 * GR; ++h) {
+        const int fa = 2 * (4 * (2 * k0 + h) + wave);
+        if (fa < nfr) {
           float *ra = tile + SPEC_LD * fa;
           float *rb = ra + SPEC_LD;
 #pragma unroll
