@@ -331,7 +331,11 @@ class PESQ(BaseMetric):
         n_bad, bad, second = alignment.realign_bad_intervals(clean, noisy, aligned, fr1, nseg, starts, sdel, lens)
         fr2 = fr1
         rows = torch.nonzero(n_bad).flatten()  # host sync: the second scoring covers these rows only
-        if rows.numel():
+        if 2 * rows.numel() > B:
+            # most rows: score the whole batch again rather than gather them (a row without an
+            # interval has second == aligned, so its frames come out as fr1's)
+            _, _, fr2 = self.frame_disturbances(clean, second, lens)
+        elif rows.numel():
             fr2 = fr1.clone()
             _, _, sub = self.frame_disturbances(clean[rows], second[rows], None if lens is None else lens[rows])
             fr2[rows] = sub

@@ -174,3 +174,78 @@ def test_random_plans_against_cpu_path(dev):
             assert abs(float(g[0][b]) - float(h[0][b])) <= 5e-3, (b, g[0][b], h[0][b])
     assert found >= len(rows) // 2, found
     assert same >= 0.8 * len(rows), same
+
+
+def test_interval_rules_on_synthetic_frames(dev):
+    """ta_bad_find / ta_bad_pool on synthetic per-frame disturbances through the C-ABI: the
+    oracle's interval rules bitwise (threshold, joining, minimum length, the cap of 16, runs up
+    to the row's last frame, rows of fewer than 20 frames and empty rows without intervals), and
+    the pooled MOS of mixed first / second frames against the float64 pooling."""
+    lib = _native.load()
+    L = 96000
+    F = lib.fsem_pesq_frames(L)
+    rng = np.random.default_rng(5)
+    B = 6
+    sym = rng.uniform(0.0, 25.0, (B, F)).astype(np.float32)
+    sym[0, 100:103] = 40.0                    # too short
+    sym[0, 200:203] = sym[0, 206:209] = 44.0  # joined across a gap of 3
+    sym[1, :] = np.tile(np.r_[np.full(5, 45.0), np.full(4, 10.0)], F // 9 + 1)[:F]  # > 16 runs: cap
+    sym[2, F - 6:] = 45.0                     # up to the last frame
+    sym[3, 10:30] = 31.0                      # a row of 3000 samples (< 20 frames): none
+    sym[4, 50:60] = 30.0                      # not above the threshold
+    lens = np.array([L, L, L, 3000, L, 0], dtype=np.int32)
+    frames = np.zeros((B, 2, F), np.float32)
+    frames[:, 0] = sym
+    frames[:, 1] = rng.uniform(0.0, 20.0, (B, F))
+    frames2 = frames.copy()
+    frames2[:, :, :] *= 0.5                   # the second scoring disturbs less everywhere
+    c = torch.from_numpy(rng.standard_normal((B, L)).astype(np.float32)).to(dev)
+    d = torch.roll(c, 40, dims=1).contiguous()
+    fr = torch.from_numpy(frames).to(dev)
+    i32 = dict(dtype=torch.int32, device=dev)
+    nseg = torch.ones(B, **i32)
+    st = torch.zeros(B, 33, **i32)
+    st[:, 1] = torch.from_numpy(lens).to(dev)
+    sd = torch.full((B, 32), 40, **i32)
+    n_bad = torch.empty(B, **i32)
+    bad = torch.zeros(B, 16, 3, **i32)
+    second = torch.empty(B, L, device=dev)
+    lt = torch.from_numpy(lens).to(dev)
+    ws = torch.empty(lib.fsem_pesq_bad_intervals_workspace_bytes(B, L), dtype=torch.uint8, device=dev)
+    assert lib.fsem_pesq_bad_intervals_f32(c.data_ptr(), d.data_ptr(), d.data_ptr(), B, L, L, lt.data_ptr(),
+                                           fr.data_ptr(), nseg.data_ptr(), st.data_ptr(), sd.data_ptr(),
+                                           n_bad.data_ptr(), bad.data_ptr(), second.data_ptr(), L, ws.data_ptr(),
+                                           ws.numel(), None) == 0
+    torch.cuda.synchronize()
+    nb, bd = n_bad.cpu().numpy(), bad.cpu().numpy()
+    want = []
+    for b in range(B):
+        Fb = lib.fsem_pesq_frames(int(lens[b]))
+        iv = A.bad_intervals(sym[b, :Fb]) if Fb >= 20 else []
+        want.append(iv)
+        assert int(nb[b]) == len(iv), (b, nb[b], iv)
+        assert [tuple(x[:2]) for x in bd[b, :len(iv)].tolist()] == iv
+    assert want[0] == [(200, 209)] and len(want[1]) == 16 and want[2] == [(F - 6, F)] and want[3] == [] == want[4]
+    # every interval's delay: the roll by 40 samples, found within +-383 of the segment's 40
+    for b in range(B):
+        for f0, f1, D in bd[b, :int(nb[b])].tolist():
+            assert D == 40, (b, f0, f1, D)
+    # pooling: interval frames from the second scoring, the rest from the first
+    dist = torch.zeros(2, B, device=dev)
+    dist[:, 5] = float("nan")
+    mos = torch.empty(B, device=dev)
+    fr2 = torch.from_numpy(frames2).to(dev)
+    assert lib.fsem_pesq_pool_f32(fr.data_ptr(), fr2.data_ptr(), dist.data_ptr(), B, L, lt.data_ptr(),
+                                  n_bad.data_ptr(), bad.data_ptr(), mos.data_ptr(), None) == 0
+    got = mos.cpu().numpy()
+    for b in range(B):
+        Fb = lib.fsem_pesq_frames(int(lens[b]))
+        if Fb < 20 or b == 5:
+            assert np.isnan(got[b])
+            continue
+        s, a = frames[b, 0, :Fb].astype(np.float64), frames[b, 1, :Fb].astype(np.float64)
+        for f0, f1 in want[b]:
+            s[f0:f1] = frames2[b, 0, f0:f1]
+            a[f0:f1] = frames2[b, 1, f0:f1]
+        ref = po.mos_from_distances(po.overlapping_sums(s[None]), po.overlapping_sums(a[None]))[0]
+        assert abs(got[b] - ref) <= 1e-6, (b, got[b], ref)
