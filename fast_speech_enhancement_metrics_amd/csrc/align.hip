@@ -34,10 +34,12 @@
 //      apart) are both more confident than the whole, the most confident pair first, and each
 //      half once more (P.862 utterance_split, two levels: up to 4 segments per utterance);
 //      ta_segments_p862: the row's segments as in stage 8, at most MAXSEG.
-// Cost is set by stage 3: 767 lags x L multiply-adds per row (about 123 M for 10 s), as
-// register-blocked packed FMAs out of LDS (16 consecutive lags per lane sliding over the chunk);
-// the other stages are O(L) or O(M * L / 64).
+// Cost was set by stage 3: 767 lags x L multiply-adds per row (about 123 M for 10 s) as
+// register-blocked packed FMAs out of LDS (ta_fine_partial); ta_fine_fft computes the same
+// partials by fast correlation (per 1280-sample block, 2048-point transforms: ~12x less work).
+// The other stages are O(L) or O(M * L / 64).
 #include "fsem_common.h"
+#include "fsem_fft.h"
 
 namespace fsem {
 namespace align {
@@ -221,6 +223,51 @@ struct UttTables {
   const int4 *desc = nullptr;
   const int *ndesc = nullptr;  // [B]
 };
+// Workgroup blk's slot: row b, slot c, samples [n0, hi) correlated at lags lag0 + j (j < 768).
+struct SlotRange {
+  bool valid;
+  int64_t b, Lr, n0, hi, lag0;
+  int c;
+};
+__device__ __forceinline__ SlotRange slot_range(int64_t blk, int64_t B, int64_t L, const int32_t *lengths,
+                                                const int *crude, int nchunk, const UttTables &ut) {
+  SlotRange r;
+  // slot descriptors (few active slots per row): rows fastest, so the active workgroups spread
+  // over the XCDs instead of landing on the few that row-major slot ids map to
+  r.b = ut.desc ? blk % B : blk / nchunk;
+  r.c = (int)(ut.desc ? blk / B : blk % nchunk);
+  r.valid = r.b < B;
+  if (!r.valid) return r;
+  r.Lr = row_len(lengths, r.b, L);
+  r.n0 = (int64_t)r.c * CS;
+  r.hi = r.n0 + CS;
+  r.lag0 = crude ? (int64_t)crude[r.b] - FINE : 0;  // crude: NULL with slot descriptors
+  if (ut.nutt) {
+    const int U = ut.nutt[r.b];
+    const int *cs = ut.cs + r.b * (MAXU + 1);
+    if (r.c >= cs[U]) {  // past the row's pieces (uniform)
+      r.valid = false;
+      return r;
+    }
+    int u = 0;
+    while (u + 1 < U && cs[u + 1] <= r.c) ++u;
+    const int *reg = ut.reg + r.b * (MAXU + 1);
+    r.n0 = (int64_t)reg[u] + (int64_t)(r.c - cs[u]) * CS;
+    r.hi = std::min<int64_t>(r.n0 + CS, reg[u + 1]);
+    r.lag0 = (int64_t)ut.ucrude[r.b * MAXU + u] - FINE;
+  } else if (ut.desc) {
+    if (r.c >= ut.ndesc[r.b]) {  // past the row's pieces (uniform)
+      r.valid = false;
+      return r;
+    }
+    const int4 d = ut.desc[r.b * nchunk + r.c];
+    r.n0 = d.x;
+    r.hi = d.y;
+    r.lag0 = (int64_t)d.z - FINE;
+  }
+  return r;
+}
+
 __global__ void __launch_bounds__(256) ta_fine_partial(const float *__restrict__ ref, const float *__restrict__ deg,
                                                        int64_t B, int64_t L, int64_t ld,
                                                        const int32_t *__restrict__ lengths,
@@ -229,32 +276,10 @@ __global__ void __launch_bounds__(256) ta_fine_partial(const float *__restrict__
   __shared__ float wr[CS];
   __shared__ float wd[WIN + WIN / 32 + 64];
   __shared__ float ps[NSL][NGRP * LG];
-  const int64_t blk = blockIdx.x;
-  // slot descriptors (few active slots per row): rows fastest, so the active workgroups spread
-  // over the XCDs instead of landing on the few that row-major slot ids map to
-  const int64_t b = ut.desc ? blk % B : blk / nchunk;
-  const int c = (int)(ut.desc ? blk / B : blk % nchunk);
-  if (b >= B) return;
-  const int64_t Lr = row_len(lengths, b, L);
-  int64_t n0 = (int64_t)c * CS, hi = n0 + CS;
-  int64_t lag0 = crude ? (int64_t)crude[b] - FINE : 0;  // crude: NULL with slot descriptors
-  if (ut.nutt) {
-    const int U = ut.nutt[b];
-    const int *cs = ut.cs + b * (MAXU + 1);
-    if (c >= cs[U]) return;  // past the row's pieces (uniform)
-    int u = 0;
-    while (u + 1 < U && cs[u + 1] <= c) ++u;
-    const int *reg = ut.reg + b * (MAXU + 1);
-    n0 = (int64_t)reg[u] + (int64_t)(c - cs[u]) * CS;
-    hi = std::min<int64_t>(n0 + CS, reg[u + 1]);
-    lag0 = (int64_t)ut.ucrude[b * MAXU + u] - FINE;
-  } else if (ut.desc) {
-    if (c >= ut.ndesc[b]) return;  // past the row's pieces (uniform)
-    const int4 d = ut.desc[b * nchunk + c];
-    n0 = d.x;
-    hi = d.y;
-    lag0 = (int64_t)d.z - FINE;
-  }
+  const SlotRange sr = slot_range(blockIdx.x, B, L, lengths, crude, nchunk, ut);
+  if (!sr.valid) return;  // uniform
+  const int64_t b = sr.b, Lr = sr.Lr, n0 = sr.n0, hi = sr.hi, lag0 = sr.lag0;
+  const int c = sr.c;
   const float *x = ref + b * ld, *y = deg + b * ld;
   const int tid = threadIdx.x;
   auto dif = [Lr](const float *z, int64_t i) {  // first difference, 0 outside [1, L_row)
@@ -311,6 +336,156 @@ __global__ void __launch_bounds__(256) ta_fine_partial(const float *__restrict__
     for (int q = 1; q < NSL; ++q) t += ps[q][j];
     part[(b * nchunk + c) * (NGRP * LG) + j] = t;
   }
+}
+
+// ---------------------------------------------------------------- stage 3, FFT form
+// The same partials as ta_fine_partial by fast correlation (FSEM_FINE_FFT): wave q of the
+// workgroup takes the slot's block q, x[i] = wr[n0 + 1280 q + i] (i < 1280 and below the slot's
+// end, else 0) and y[i] = wd[n0 + 1280 q + lag0 + i] (i < 2048); its c_q[j] = sum_i x[i] y[i + j]
+// (j < 768) is their circular correlation of length 2048 (no wrap: 1280 + 767 < 2048):
+//   Z = FFT(x + i y) -- four 512-point transforms of the samples 4n + r (fft512_wave_x2) and a
+//   radix-4 step -- then with A = Z[k] + conj Z[-k], B = Z[k] - conj Z[-k]:
+//   X = A / 2, Y = B / 2i, and c = Re IFFT(conj(X) Y) = Re FFT(X conj(Y)) / 2048 with
+//   X conj(Y) = i A conj(B) / 4 (one more four-transform FFT, after a transposition through the
+//   wave's LDS area).  The four blocks' c_q are added in block order.  The values differ from the
+//   direct sums by float32 rounding (both forms: ~1e-7 .. 1e-6 of |x| |y|); the work per slot is
+//   ~12x smaller.
+constexpr int FB = 1280;  // samples of x per block (wave)
+constexpr int FN = 2048;  // transform length
+static_assert(4 * FB == CS && FB + NGRP * LG - 1 <= FN, "four blocks per slot; no wrap");
+
+__device__ __forceinline__ cf w2048(int t) {  // exp(-2 pi i t / 2048), 0 <= t < 2048
+  // W_512^(t >> 2) from the 512-point table times W_2048^(t & 3)
+  const float fr[4] = {1.0f, 0.9999953f, 0.99998116f, 0.9999576f};
+  const float fi[4] = {-0.0f, -0.0030679568f, -0.0061358847f, -0.009203754f};
+  const int f = t & 3;
+  return cmul(cf{kTwRe[t >> 2], kTwIm[t >> 2]}, cf{fr[f], fi[f]});
+}
+
+__global__ void __launch_bounds__(256) ta_fine_fft(const float *__restrict__ ref, const float *__restrict__ deg,
+                                                   int64_t B, int64_t L, int64_t ld,
+                                                   const int32_t *__restrict__ lengths,
+                                                   const int *__restrict__ crude, int nchunk,
+                                                   float *__restrict__ part, UttTables ut) {
+  __shared__ __attribute__((aligned(16))) float2 fbuf[4][FN];  // per wave: exchange + transposition
+  const SlotRange sr = slot_range(blockIdx.x, B, L, lengths, crude, nchunk, ut);
+  if (!sr.valid) return;  // uniform
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float2 *buf = fbuf[wave];
+  const float *xr = ref + sr.b * ld, *yd = deg + sr.b * ld;
+  const int64_t Lr = sr.Lr;
+  const int64_t xb = sr.n0 + (int64_t)FB * wave;  // block start (x)
+  const int64_t yb = xb + sr.lag0;                // window start (y)
+  const int64_t xend = std::min<int64_t>(sr.hi, xb + FB);
+  float cq[12];  // c_q at lags lane + 64 m
+  if (xend > xb) {  // uniform
+    cf tw1[8], tw2[8];
+    fft512_twiddles(lane, tw1, tw2);
+    // subsequence r's element n = lane + 64 s is z[4 n + r] = z[4 lane + 256 s + r]
+    cf g[4][8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int i0 = 4 * lane + 256 * s;
+      float xv[5], yv[5];  // samples i0 - 1 .. i0 + 3 of the block and the window
+#pragma unroll
+      for (int e = 0; e < 5; ++e) {
+        const int64_t tx = xb + i0 - 1 + e, ty = yb + i0 - 1 + e;
+        xv[e] = (tx >= 0 && tx < Lr) ? xr[tx] : 0.f;
+        yv[e] = (ty >= 0 && ty < Lr) ? yd[ty] : 0.f;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t tx = xb + i0 + r, ty = yb + i0 + r;
+        // first differences, 0 outside [1, L_row) (ta_fine_partial's dif), x also past the slot
+        const float dx = (i0 + r < FB && tx < xend && tx >= 1 && tx < Lr) ? xv[r + 1] - xv[r] : 0.f;
+        const float dy = (ty >= 1 && ty < Lr) ? yv[r + 1] - yv[r] : 0.f;
+        g[r][s] = {dx, dy};
+      }
+    }
+    cf t4[3][8];  // radix-4 twiddles W_2048^(r k0), k0 = lane + 64 j
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int r = 1; r < 4; ++r) t4[r - 1][j] = w2048((r * (lane + 64 * j)) & (FN - 1));
+    fft512_wave_x2(g[0], g[1], buf, lane, tw1, tw2);
+    fft512_wave_x2(g[2], g[3], buf, lane, tw1, tw2);
+    cf Z[32];  // Z[lane + 64 m]
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const cf a0 = g[0][j], a1 = cmul(g[1][j], t4[0][j]), a2 = cmul(g[2][j], t4[1][j]),
+               a3 = cmul(g[3][j], t4[2][j]);
+      const cf s02 = cadd(a0, a2), d02 = csub(a0, a2), s13 = cadd(a1, a3), d13 = mul_mi(csub(a1, a3));
+      Z[j] = cadd(s02, s13);
+      Z[j + 8] = cadd(d02, d13);
+      Z[j + 16] = csub(s02, s13);
+      Z[j + 24] = csub(d02, d13);
+    }
+    // Q = i A conj(B): conj Z[-k] from lane 64 - lane, register 31 - m (lane 0: (32 - m) mod 32)
+    const int plane = (64 - lane) & 63;
+    cf Q[32];
+#pragma unroll
+    for (int m = 0; m < 32; ++m) {
+      float mr = __shfl(Z[31 - m].r, plane, 64);
+      float mi = __shfl(Z[31 - m].i, plane, 64);
+      if (lane == 0) {
+        mr = Z[(32 - m) & 31].r;
+        mi = Z[(32 - m) & 31].i;
+      }
+      const cf A = {Z[m].r + mr, Z[m].i - mi}, Bv = {Z[m].r - mr, Z[m].i + mi};
+      const cf P = {fmaf(A.r, Bv.r, A.i * Bv.i), fmaf(A.i, Bv.r, -(A.r * Bv.i))};  // A conj(B)
+      Q[m] = {-P.i, P.r};
+    }
+#pragma unroll
+    for (int m = 0; m < 32; ++m) buf[lane + 64 * m] = make_float2(Q[m].r, Q[m].i);
+    wave_lds_fence();
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const float4 *q4 = reinterpret_cast<const float4 *>(buf + 4 * lane + 256 * s);
+      const float4 u = q4[0], v = q4[1];
+      g[0][s] = {u.x, u.y};
+      g[1][s] = {u.z, u.w};
+      g[2][s] = {v.x, v.y};
+      g[3][s] = {v.z, v.w};
+    }
+    fft512_wave_x2(g[0], g[1], buf, lane, tw1, tw2);
+    fft512_wave_x2(g[2], g[3], buf, lane, tw1, tw2);
+    constexpr float kScale = 1.f / (4.f * FN);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const cf a0 = g[0][j], a1 = cmul(g[1][j], t4[0][j]), a2 = cmul(g[2][j], t4[1][j]),
+               a3 = cmul(g[3][j], t4[2][j]);
+      cq[j] = ((a0.r + a2.r) + (a1.r + a3.r)) * kScale;  // k0
+      if (j < 4) cq[8 + j] = ((a0.r - a2.r) + (a1.i - a3.i)) * kScale;  // k0 + 512: Re(d02 - i d13)
+    }
+  } else {
+#pragma unroll
+    for (int m = 0; m < 12; ++m) cq[m] = 0.f;
+  }
+  wave_lds_fence();  // the last transform's reads of buf are done
+  float *cb = reinterpret_cast<float *>(buf);
+#pragma unroll
+  for (int m = 0; m < 12; ++m) cb[lane + 64 * m] = cq[m];
+  __syncthreads();
+  const float *c0 = reinterpret_cast<const float *>(fbuf[0]), *c1 = reinterpret_cast<const float *>(fbuf[1]),
+              *c2 = reinterpret_cast<const float *>(fbuf[2]), *c3 = reinterpret_cast<const float *>(fbuf[3]);
+  for (int j = tid; j < NGRP * LG; j += 256)
+    part[(sr.b * nchunk + sr.c) * (NGRP * LG) + j] = ((c0[j] + c1[j]) + c2[j]) + c3[j];
+}
+
+// the fine stage's partials of every slot: the FFT form (default), or the direct one
+// (FSEM_FINE_FFT=0, kept for A/B): 4096 x 10 s PESQ with row / utterance / P.862-mode alignment
+// 19.3 / 26.6 / 45.7 ms direct, 11.2 / 13.8 / 28.8 ms FFT, every synthetic delay recovered by both
+// (profiles/r6_g/ab_fine_fft.txt)
+#ifndef FSEM_FINE_FFT
+#define FSEM_FINE_FFT 1
+#endif
+inline void launch_fine(unsigned grid, hipStream_t st, const float *ref, const float *deg, int64_t B, int64_t L,
+                        int64_t ld, const int32_t *lengths, const int *crude, int nchunk, float *part,
+                        const UttTables &ut) {
+  if (FSEM_FINE_FFT)
+    ta_fine_fft<<<grid, 256, 0, st>>>(ref, deg, B, L, ld, lengths, crude, nchunk, part, ut);
+  else
+    ta_fine_partial<<<grid, 256, 0, st>>>(ref, deg, B, L, ld, lengths, crude, nchunk, part, ut);
 }
 
 // ---------------------------------------------------------------- stage 3b: fine delay
@@ -1314,8 +1489,8 @@ extern "C" int fsem_time_align_f32(const float *ref, const float *deg, int64_t b
   FSEM_CHECK_LAUNCH();
   align::ta_crude<<<xy(batch), 256, 0, st>>>(batch, length, lengths, w.E, nfr_cap, max_frames, w.crude);
   FSEM_CHECK_LAUNCH();
-  align::ta_fine_partial<<<(unsigned)(batch * nch), 256, 0, st>>>(ref, deg, batch, length, ld, lengths, w.crude,
-                                                                  (int)nch, w.part, align::UttTables{});
+  align::launch_fine((unsigned)(batch * nch), st, ref, deg, batch, length, ld, lengths, w.crude, (int)nch, w.part,
+                     align::UttTables{});
   FSEM_CHECK_LAUNCH();
   align::ta_fine_pick<<<xy(batch), 256, 0, st>>>(batch, w.crude, (int)nch, w.part, dl);
   FSEM_CHECK_LAUNCH();
@@ -1377,8 +1552,8 @@ static int time_align_segmented(bool p862, const float *ref, const float *deg, i
                                               w.utt, w.ucrude);
     FSEM_CHECK_LAUNCH();
   }
-  align::ta_fine_partial<<<(unsigned)(batch * nsl), 256, 0, st>>>(
-      ref, deg, batch, length, ld, lengths, w.crude, (int)nsl, w.part, align::UttTables{w.nutt, w.reg, w.cs, w.ucrude});
+  align::launch_fine((unsigned)(batch * nsl), st, ref, deg, batch, length, ld, lengths, w.crude, (int)nsl, w.part,
+                     align::UttTables{w.nutt, w.reg, w.cs, w.ucrude});
   FSEM_CHECK_LAUNCH();
   if (p862) {
     const align::P862Ws q = align::p862_carve(ws, batch, length);
@@ -1459,8 +1634,8 @@ extern "C" int fsem_pesq_bad_intervals_f32(const float *ref, const float *deg, c
   align::UttTables ut{};
   ut.desc = w.desc;
   ut.ndesc = w.ndesc;
-  align::ta_fine_partial<<<(unsigned)(batch * nsl), 256, 0, st>>>(ref, deg, batch, length, ld, lengths, nullptr,
-                                                                  (int)nsl, w.part, ut);
+  align::launch_fine((unsigned)(batch * nsl), st, ref, deg, batch, length, ld, lengths, nullptr, (int)nsl, w.part,
+                     ut);
   FSEM_CHECK_LAUNCH();
   {
     const dim3 grid((unsigned)std::min<int64_t>(batch, 65535), align::MAXBAD, (unsigned)((batch + 65534) / 65535));

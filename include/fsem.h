@@ -219,7 +219,7 @@ int fsem_pesq_stoi_f32(const float *ref, const float *deg, int64_t batch, int64_
  *                 16-byte aligned rows):
  *                 deg_aligned[b][n] = deg[b][n + D] where 0 <= n + D < lengths[b], else 0
  *                 (not in place: deg_aligned must not overlap deg)
- * Cost: about 767 multiply-adds per sample (the fine search); see csrc/align.hip.
+ * Cost: dominated by the fine search (fast correlation per 1280-sample block); see csrc/align.hip.
  */
 size_t fsem_time_align_workspace_bytes(int64_t batch, int64_t length);
 int fsem_time_align_f32(const float *ref, const float *deg, int64_t batch, int64_t length,
