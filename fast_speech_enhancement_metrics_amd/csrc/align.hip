@@ -168,15 +168,21 @@ __global__ void __launch_bounds__(256) ta_crude(int64_t B, int64_t L, const int3
     }
   }
   __syncthreads();
-  const float *r = in_lds ? er : gr;
-  const float *d = in_lds ? ed : gd;
   const int M = nfr < 2 ? 0 : min(max_frames, nfr - 1);
   float best = 0.f;
   int arg = 0;
   for (int j = -M + tid; j <= M; j += 256) {
     const int k0 = j < 0 ? -j : 0, k1 = j < 0 ? nfr : nfr - j;
     float c = 0.f;
-    for (int k = k0; k < k1; ++k) c = fmaf(r[k], d[k + j], c);
+    // two loops, not one over a selected pointer (flat loads), unrolled by 8: eight loads in
+    // flight per wait, the chain of fmaf in the same order (as ta_crude_utt)
+    if (in_lds) {
+#pragma unroll 8
+      for (int k = k0; k < k1; ++k) c = fmaf(er[k], ed[k + j], c);
+    } else {
+#pragma unroll 8
+      for (int k = k0; k < k1; ++k) c = fmaf(gr[k], gd[k + j], c);
+    }
     if (c > best) {  // j ascending per thread: the first maximum is kept
       best = c;
       arg = j;

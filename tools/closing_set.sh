@@ -9,7 +9,8 @@
 #   3. bench.py, the driver's command                                   -> bench.json
 #   4. bench.py under rocprofv3 --kernel-trace --stats (its pesq_front average must agree with
 #      the bench line's roofline.ms_per_launch) and the per-step timeline -> trace_bench/, timeline_bench.txt
-#   5. the other configurations' lines (PESQ alone, config 3, config 5)  -> bench_{pesq,c3,c5}.json
+#   5. the other configurations' lines (PESQ alone, config 3, config 5, PESQ with the three
+#      time-alignment modes)                                         -> bench_{pesq,c3,c5,pesq_aligned*}.json
 #   6. smoke()                                                          -> smoke.txt
 # Every GPU step runs under its own time limit and the chain stops at the first failure.  The
 # ISA statistics of the same build come from the CPU side (tools/isa_stats.py, see README).
@@ -41,7 +42,7 @@ cd /tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/trace_bench -o run --output-format csv -- python $R/bench.py --no-cpu-baseline > $OUT/bench_traced.json 2> $OUT/trace.log || { echo "TRACE FAILED"; tail -20 $OUT/trace.log; exit 1; }
 cd $R
 python tools/timeline.py $OUT/trace_bench > $OUT/timeline_bench.txt 2>&1 || exit 1
-for w in pesq c3 c5; do
+for w in pesq c3 c5 pesq_aligned pesq_aligned_utt pesq_aligned_p862; do
   timeout -k 10 300 python bench.py --workload $w --no-cpu-baseline > $OUT/bench_$w.json 2> $OUT/bench_$w.err || { echo "BENCH $w FAILED"; exit 1; }
 done
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.txt 2>&1 || { echo "SMOKE FAILED"; tail $OUT/smoke.txt; exit 1; }
