@@ -28,6 +28,30 @@ def _unit_rows(x: torch.Tensor, lengths=None) -> torch.Tensor:
     return x * torch.exp2(-ex).to(x.dtype)[:, None]  # a power of two: exact, as ldexp
 
 
+def _wb_frames(lib, clean: torch.Tensor, noisy: torch.Tensor, lens):
+    """(distances [2, B], per-frame disturbances [B, 2, F]) of 16 kHz rows on the GPU through the
+    whole-metric entry (fsem_pesq_wb_frames_f32: its range handling, no host-side row scaling)."""
+    clean = as_rows(clean)
+    noisy = as_rows(noisy)
+    B, L = clean.shape
+    F = lib.fsem_pesq_frames(L)
+    if F < 20 and lens is None:
+        raise RuntimeError(f"maximum size for tensor at dimension 1 is {max(F, 0)} but size is 20")
+    if clean.stride(0) != noisy.stride(0) or L % 4 or not (clean.is_contiguous() and noisy.is_contiguous()):
+        pad = (-L) % 4
+        clean = torch.nn.functional.pad(clean, (0, pad)).contiguous()
+        noisy = torch.nn.functional.pad(noisy, (0, pad)).contiguous()
+    mos = torch.empty(B, dtype=torch.float32, device=clean.device)
+    dist = torch.empty(2, B, dtype=torch.float32, device=clean.device)
+    frames = torch.full((B, 2, F), float("nan"), device=clean.device)
+    ws = _native.workspace(lib.fsem_pesq_workspace_bytes(B, L), clean.device)
+    _native.check(lib.fsem_pesq_wb_frames_f32(clean.data_ptr(), noisy.data_ptr(), B, L, clean.stride(0),
+                                              lens.data_ptr() if lens is not None else None, mos.data_ptr(),
+                                              dist.data_ptr(), frames.data_ptr(), ws.data_ptr(), ws.numel(),
+                                              _native.stream_handle(clean.device)), "PESQ frames")
+    return dist[0], frames
+
+
 class PESQ(BaseMetric):
     higher_is_better = True
     EXPECTED_SAMPLING_RATE = 16000
@@ -327,17 +351,17 @@ class PESQ(BaseMetric):
         lib = _native.load()
         lens = device_lengths(lengths, B, L, clean.device) if lengths is not None else None
         aligned, delays, nseg, starts, sdel = alignment.time_align_segments(clean, noisy, lens, max_delay, mode="p862")
-        ds, _, fr1 = self.frame_disturbances(clean, aligned, lens)
+        ds, fr1 = _wb_frames(lib, clean, aligned, lens)
         n_bad, bad, second = alignment.realign_bad_intervals(clean, noisy, aligned, fr1, nseg, starts, sdel, lens)
         fr2 = fr1
         rows = torch.nonzero(n_bad).flatten()  # host sync: the second scoring covers these rows only
         if 2 * rows.numel() > B:
             # most rows: score the whole batch again rather than gather them (a row without an
             # interval has second == aligned, so its frames come out as fr1's)
-            _, _, fr2 = self.frame_disturbances(clean, second, lens)
+            _, fr2 = _wb_frames(lib, clean, second, lens)
         elif rows.numel():
             fr2 = fr1.clone()
-            _, _, sub = self.frame_disturbances(clean[rows], second[rows], None if lens is None else lens[rows])
+            _, sub = _wb_frames(lib, clean[rows], second[rows], None if lens is None else lens[rows])
             fr2[rows] = sub
         mos = torch.empty(B, dtype=torch.float32, device=clean.device)
         _native.check(lib.fsem_pesq_pool_f32(fr1.data_ptr(), fr2.data_ptr(), ds.data_ptr(), B, L,

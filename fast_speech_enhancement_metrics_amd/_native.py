@@ -71,6 +71,8 @@ SIGNATURES = {
     "fsem_pesq_bad_intervals_f32": (ctypes.c_int, [_vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp,
                                                     _vp, _vp, _vp, _c_i64, _vp, _c_sz, _vp]),
     "fsem_pesq_pool_f32": (ctypes.c_int, [_vp, _vp, _vp, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp]),
+    "fsem_pesq_wb_frames_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _c_sz,
+                                               _vp]),
 }
 ALIGN_MAX_SEGMENTS = 32  # include/fsem.h FSEM_ALIGN_MAX_SEGMENTS
 PESQ_MAX_BAD = 16  # include/fsem.h FSEM_PESQ_MAX_BAD

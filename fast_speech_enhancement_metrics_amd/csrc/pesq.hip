@@ -1451,3 +1451,18 @@ extern "C" int fsem_pesq_wb_f32(const float *ref, const float *deg, int64_t batc
   return pesq::run_wb(ref, deg, batch, length, ld, lengths, mos, ws, ws_bytes, nullptr, 0, nullptr, 0,
                        (hipStream_t)stream, (hipStream_t)stream);
 }
+
+// The whole-metric path with the back end's intermediates (ABI 10): the front end with its range
+// handling (no host-side row scaling, which the stage entries need), then the back end's
+// distances and per-frame disturbances beside the scores.
+extern "C" int fsem_pesq_wb_frames_f32(const float *ref, const float *deg, int64_t batch, int64_t length,
+                                       int64_t ld, const int32_t *lengths, float *mos, float *dist, float *frames,
+                                       void *ws, size_t ws_bytes, void *stream) {
+  if (!mos || !dist || !frames) return FSEM_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  const int rc = pesq::run_wb_front(ref, deg, batch, length, ld, lengths, ws, ws_bytes, nullptr, 0, nullptr, 0, st);
+  if (rc != FSEM_OK) return rc;
+  const WbWs w = carve_wb(ws, batch, length);
+  return pesq::launch_back(w.bark, nullptr, static_cast<const float *>(ws), batch, length, lengths, mos, w.back,
+                           fsem_pesq_back_workspace_bytes(batch, length), st, dist, frames);
+}

@@ -1000,7 +1000,7 @@ extern "C" const char *fsem_strerror(int code) {
   }
 }
 
-extern "C" int fsem_version(void) { return 9; }  // 9: + fsem_pesq_bad_intervals_*, fsem_pesq_pool_f32; 8: + fsem_time_align_p862_*; 7: + fsem_host_buffer_mapped; 6: + fsem_build_id; 5: + fsem_time_align_utt_*; 4: + fsem_pre_emphasize_f32; 3: + fsem_time_align_*, fsem_pesq_distances_*
+extern "C" int fsem_version(void) { return 10; }  // 10: + fsem_pesq_wb_frames_f32; 9: + fsem_pesq_bad_intervals_*, fsem_pesq_pool_f32; 8: + fsem_time_align_p862_*; 7: + fsem_host_buffer_mapped; 6: + fsem_build_id; 5: + fsem_time_align_utt_*; 4: + fsem_pre_emphasize_f32; 3: + fsem_time_align_*, fsem_pesq_distances_*
 
 // The build's content hash (_build.py passes -DFSEM_BUILD_ID); the marker prefix lets the host
 // layer read the id from the file without loading it (_build.library_build_id).

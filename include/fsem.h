@@ -63,7 +63,7 @@ extern "C" {
 #define FSEM_ERATE -5         /* unsupported sample-rate pair (see resampling)      */
 
 const char *fsem_strerror(int code);
-int fsem_version(void);  /* 9: + fsem_pesq_bad_intervals_*, fsem_pesq_pool_f32; 8: + fsem_time_align_p862_*; 7: + fsem_host_buffer_mapped; 6: + fsem_build_id; 5: + fsem_time_align_utt_*; 4: + fsem_pre_emphasize_f32; 3: time alignment, distances */
+int fsem_version(void);  /* 10: + fsem_pesq_wb_frames_f32; 9: + fsem_pesq_bad_intervals_*, fsem_pesq_pool_f32; 8: + fsem_time_align_p862_*; 7: + fsem_host_buffer_mapped; 6: + fsem_build_id; 5: + fsem_time_align_utt_*; 4: + fsem_pre_emphasize_f32; 3: time alignment, distances */
 /* Content hash (16 hex digits) of the sources, headers and compile flags this library was built
  * from (fast_speech_enhancement_metrics_amd/_build.py source_hash); the host layer refuses a
  * library whose id differs from its own tree's.  "unknown" for builds outside _build.py. */
@@ -164,6 +164,15 @@ size_t fsem_pesq_distances_workspace_bytes(int64_t batch, int64_t length);
 int fsem_pesq_distances_f32(const float *bark, const float *power, int64_t batch, int64_t length,
                             const int32_t *lengths, float *dist, float *frames, void *ws,
                             size_t ws_bytes, void *stream);
+/* wb_frames (ABI 10): fsem_pesq_wb_f32 with the distances and per-frame disturbances of
+ *        fsem_pesq_distances_f32 beside the scores (dist [2, batch], frames [batch, 2, Fcap] as
+ *        there), from the rows as given: the whole-metric path's range handling, where the
+ *        stage entries need rows of moderate range.  Workspace: fsem_pesq_workspace_bytes.
+ *        Used by the P.862 mode's bad-interval realignment (fsem_pesq_bad_intervals_f32).
+ */
+int fsem_pesq_wb_frames_f32(const float *ref, const float *deg, int64_t batch, int64_t length,
+                            int64_t ld, const int32_t *lengths, float *mos, float *dist, float *frames,
+                            void *ws, size_t ws_bytes, void *stream);
 
 /* ---------------------------------------------------------------- STOI / ESTOI
  * Whole-metric entry: replaces STOI.compute_stoi + compute_metric

@@ -249,3 +249,32 @@ def test_interval_rules_on_synthetic_frames(dev):
             a[f0:f1] = frames2[b, 1, f0:f1]
         ref = po.mos_from_distances(po.overlapping_sums(s[None]), po.overlapping_sums(a[None]))[0]
         assert abs(got[b] - ref) <= 1e-6, (b, got[b], ref)
+
+
+def test_wb_frames_entry_matches_stage_entries(run, dev):
+    """fsem_pesq_wb_frames_f32 (the whole-metric path with the back end's intermediates, which the
+    P.862 chain scores with): its scores are fsem_pesq_wb_f32's, and its distances and per-frame
+    disturbances those of the stage entries (fsem_pesq_front_f32 + fsem_pesq_distances_f32 on
+    unit-scaled rows) -- also for rows scaled by 1e-6 and 1e6, which the whole-metric path takes
+    as they are."""
+    from fast_speech_enhancement_metrics_amd.PESQ import _wb_frames
+    lib = _native.load()
+    m = PESQ(16000, use_gpu=True)
+    ct, al = run["ct"], run["aligned"].contiguous()
+    for sc in (1.0, 1e-6, 1e6):
+        c, a = ct * sc, al * sc
+        ds, fr = _wb_frames(lib, c, a, None)
+        ds2, _, fr2 = m.frame_disturbances(c, a)
+        torch.testing.assert_close(fr, fr2, rtol=2e-6, atol=0)
+        torch.testing.assert_close(ds, ds2, rtol=2e-6, atol=0)
+        B, L = c.shape
+        mos = torch.empty(B, device=dev)
+        dist = torch.empty(2, B, device=dev)
+        frames = torch.empty(B, 2, lib.fsem_pesq_frames(L), device=dev)
+        ws = _native.workspace(lib.fsem_pesq_workspace_bytes(B, L), dev)
+        assert lib.fsem_pesq_wb_frames_f32(c.data_ptr(), a.data_ptr(), B, L, L, None, mos.data_ptr(),
+                                           dist.data_ptr(), frames.data_ptr(), ws.data_ptr(), ws.numel(),
+                                           None) == 0
+        torch.testing.assert_close(mos, m.scores(c, a), rtol=0, atol=0)
+    assert lib.fsem_pesq_wb_frames_f32(ct.data_ptr(), al.data_ptr(), 4, AC.L_UTT, AC.L_UTT, None, None, None,
+                                       None, None, 0, None) == _native.FSEM_EINVAL
