@@ -285,8 +285,9 @@ int fsem_time_align_p862_f32(const float *ref, const float *deg, int64_t batch, 
  * 10.7, restated in oracle/align_oracle.py steps 13-15; parity against P.862 implementations
  * unpinned), for the P.862 mode's rows.  Replaces nothing in the reference.
  *   deg_aligned : [batch, length] float32 (row stride ld_out): fsem_time_align_p862_f32's output
- *   frames      : [batch, 2, Fcap] float32 (Fcap = fsem_pesq_frames(length)):
- *                 fsem_pesq_distances_f32's per-frame disturbances of (ref, deg_aligned)
+ *   frames      : [batch, 2, Fcap] float32 (Fcap = fsem_pesq_frames(length)): the per-frame
+ *                 disturbances of (ref, deg_aligned), fsem_pesq_wb_frames_f32's (or
+ *                 fsem_pesq_distances_f32's)
  *   n_seg, seg_start, seg_delay : that alignment's segments
  *   n_bad       : [batch] int32 output: intervals per row (0 .. FSEM_PESQ_MAX_BAD)
  *   bad         : [batch, FSEM_PESQ_MAX_BAD, 3] int32 output: {first frame, end frame, delay} --
