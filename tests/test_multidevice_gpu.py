@@ -71,8 +71,9 @@ def test_ragged_rows_balanced_by_length(pairs):
 
 
 def test_other_rate_and_time_alignment(pairs):
-    """8 kHz rows (PESQ 8->16 kHz, STOI 8->10 kHz per shard) and PESQ(time_align=True): delays
-    and scores reassembled in row order."""
+    """8 kHz rows (PESQ 8->16 kHz, STOI 8->10 kHz per shard) and PESQ with each time-alignment
+    mode (row, utterance, P.862 with its bad-interval rescoring per shard): delays and scores
+    reassembled in row order, bitwise the single-device call's."""
     from fast_speech_enhancement_metrics_amd import PESQ, PESQ_STOI
     from fast_speech_enhancement_metrics_amd.synthetic import speech_like_pairs
     c8, n8, _ = speech_like_pairs(10, 24000, 8000, seed=62, device="cuda")
@@ -85,11 +86,12 @@ def test_other_rate_and_time_alignment(pairs):
     t = torch.arange(c.shape[1], device="cuda")
     src = t[None, :] - D[:, None]
     deg = torch.where((src >= 0) & (src < c.shape[1]), n.gather(1, src.clamp(0, c.shape[1] - 1)), torch.zeros_like(n))
-    a1 = PESQ(16000, use_gpu=True, time_align=True)
-    want = a1.scores(c, deg).cpu().numpy()
-    a2 = PESQ(16000, use_gpu=True, time_align=True, devices=[0, 0])
-    np.testing.assert_array_equal(a2.scores(c, deg).cpu().numpy(), want)
-    np.testing.assert_array_equal(a2.last_delays.cpu().numpy(), a1.last_delays.cpu().numpy())
+    for mode in (True, "utterance", "p862"):
+        a1 = PESQ(16000, use_gpu=True, time_align=mode)
+        want = a1.scores(c, deg).cpu().numpy()
+        a2 = PESQ(16000, use_gpu=True, time_align=mode, devices=[0, 0])
+        np.testing.assert_array_equal(a2.scores(c, deg).cpu().numpy(), want)
+        np.testing.assert_array_equal(a2.last_delays.cpu().numpy(), a1.last_delays.cpu().numpy())
 
 
 def test_streams_overlap_and_caller_stream_order(pairs):
