@@ -11,7 +11,7 @@ import torch
 
 from . import _cpu, _native
 from .bark import BarkFilterBank
-from .base import BaseMetric, as_rows, check_row_rate, device_lengths, noisy_shape, resample_rows
+from .base import BaseMetric, as_rows, check_row_rate, device_lengths, noisy_shape, resample_rows, same_device
 from .loudness import Loudness
 from .spectrogram import Spectrogram
 
@@ -233,6 +233,7 @@ class PESQ(BaseMetric):
         fsem_pesq_distances_f32); rows under 20 frames give NaN distances."""
         # each signal is level-aligned on its own (PESQ.py:92-102), so scaling a row by a power of
         # two changes nothing but the range: rows go in with peaks in [1, 2), as _front
+        same_device(as_rows(clean_speech), as_rows(noisy_speech))
         clean = _unit_rows(as_rows(clean_speech), lengths)
         noisy = _unit_rows(as_rows(noisy_speech), lengths)
         lib = _native.load()
@@ -303,6 +304,7 @@ class PESQ(BaseMetric):
         B, L = clean.shape
         if noisy.shape != clean.shape:
             raise Exception("`clean_speech` and `denoised_speech` should have the same shape.")
+        same_device(clean, noisy)
         if getattr(self, "time_align", False) == "p862":
             mos, delays, _, _ = self.p862_scores(clean, noisy, lengths)
             return mos, delays
@@ -343,6 +345,7 @@ class PESQ(BaseMetric):
         from . import alignment
         clean = as_rows(clean_speech)
         noisy = as_rows(noisy_speech)
+        same_device(clean, noisy)
         B, L = clean.shape
         max_delay = getattr(self, "max_delay", alignment.DEFAULT_MAX_DELAY)
         if not clean.is_cuda:

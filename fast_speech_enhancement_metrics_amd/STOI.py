@@ -13,7 +13,7 @@ import numpy as np
 import torch
 
 from . import _cpu, _native
-from .base import BaseMetric, as_rows, check_row_rate, device_lengths, noisy_shape, zero_tail
+from .base import BaseMetric, as_rows, check_row_rate, device_lengths, noisy_shape, same_device, zero_tail
 from .batching import resampled_lengths
 
 
@@ -170,6 +170,7 @@ class STOI(BaseMetric):
         noisy = as_rows(denoised_speech)
         if noisy.shape != clean.shape:
             raise Exception("`clean_speech` and `denoised_speech` should have the same shape.")
+        same_device(clean, noisy)
         B, L = clean.shape
         if not clean.is_cuda:
             if lengths is not None:

@@ -38,7 +38,7 @@ from __future__ import annotations
 import torch
 
 from . import _cpu, _native
-from .base import as_rows, device_lengths
+from .base import as_rows, device_lengths, same_device
 
 DEFAULT_MAX_DELAY = 16000  # samples at 16 kHz (1 s)
 
@@ -51,6 +51,7 @@ def _prepare(clean, noisy, max_delay):
     n = as_rows(noisy)
     if c.shape != n.shape:
         raise Exception("`clean_speech` and `denoised_speech` should have the same shape.")
+    same_device(c, n)
     if max_delay < 0:
         raise ValueError("max_delay must be >= 0")
     return c, n, min(int(max_delay), 2**31 - 1)  # the C-ABI's int32
@@ -154,20 +155,28 @@ def realign_bad_intervals(clean: torch.Tensor, noisy: torch.Tensor, aligned: tor
         raise RuntimeError("realign_bad_intervals: GPU rows only (the CPU path is _cpu.pesq_p862)")
     B, L = c.shape
     lib = _native.load()
+    F = lib.fsem_pesq_frames(L)
+    S = _native.ALIGN_MAX_SEGMENTS
+    # the kernels index these by row, frame and segment: shapes checked before any launch, every
+    # operand moved to the rows' device
+    want = {"aligned": (aligned, (B, L)), "frames": (frames, (B, 2, F)), "n_seg": (n_seg, (B,)),
+            "seg_start": (seg_start, (B, S + 1)), "seg_delay": (seg_delay, (B, S))}
+    for name, (t, shape) in want.items():
+        if tuple(t.shape) != shape:
+            raise ValueError(f"{name} must have shape {list(shape)}, got {list(t.shape)}")
     lens = device_lengths(lengths, B, L, c.device) if lengths is not None else None
     c, n = _device_rows(c, n)
-    F = lib.fsem_pesq_frames(L)
-    frames = frames.float().contiguous()
-    if tuple(frames.shape) != (B, 2, F):
-        raise ValueError(f"frames must be [B, 2, {F}]")
-    a = aligned.float()
-    if a.stride(1) != 1 or a.stride(0) % 4 or a.data_ptr() % 16 or a.shape != (B, L):
+    frames = frames.to(device=c.device, dtype=torch.float32).contiguous()
+    a = aligned.to(device=c.device, dtype=torch.float32)
+    if a.stride(1) != 1 or a.stride(0) % 4 or a.stride(0) < L or a.data_ptr() % 16:
         a = torch.nn.functional.pad(a.contiguous(), (0, (-L) % 4))[:, :L]
     second = torch.empty(B, a.stride(0), dtype=torch.float32, device=c.device)[:, :L]
     i32 = dict(dtype=torch.int32, device=c.device)
     n_bad = torch.empty(B, **i32)
     bad = torch.zeros(B, _native.PESQ_MAX_BAD, 3, **i32)
     segs = [t.to(**i32).contiguous() for t in (n_seg, seg_start, seg_delay)]
+    if B and (int(segs[0].min()) < 0 or int(segs[0].max()) > S):
+        raise ValueError(f"n_seg must lie in [0, {S}]")
     ws = _native.workspace(lib.fsem_pesq_bad_intervals_workspace_bytes(B, L), c.device)
     _native.check(lib.fsem_pesq_bad_intervals_f32(c.data_ptr(), n.data_ptr(), a.data_ptr(), B, L, c.stride(0),
                                                   lens.data_ptr() if lens is not None else None, frames.data_ptr(),

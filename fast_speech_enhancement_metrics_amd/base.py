@@ -151,9 +151,19 @@ def zero_tail(x: torch.Tensor | None, lengths: torch.Tensor) -> torch.Tensor | N
 def device_lengths(lengths, batch: int, capacity: int, device) -> torch.Tensor:
     """Validated int32 per-row lengths on `device` (the C-ABI's `lengths` array)."""
     if isinstance(lengths, torch.Tensor) and lengths.is_cuda and lengths.dtype == torch.int32 \
-            and lengths.numel() == batch:
-        return lengths.contiguous()  # trusted device array: no host round trip
+            and lengths.numel() == batch and lengths.device == torch.device(device):
+        # trusted device array on the rows' device: no host round trip (the kernels clamp each
+        # length to [0, L])
+        return lengths.contiguous()
     return as_lengths(lengths, batch, capacity).to(device)
+
+
+def same_device(clean: torch.Tensor, noisy: torch.Tensor) -> None:
+    """The engine reads both operands on one device, as torch's own ops in the reference require
+    (a host pointer handed to a kernel would fault the GPU instead of raising)."""
+    if clean.device != noisy.device:
+        raise RuntimeError("Expected all tensors to be on the same device, but found at least two devices, "
+                           f"{clean.device} and {noisy.device}!")
 
 
 def as_rows(x: torch.Tensor) -> torch.Tensor:

@@ -18,7 +18,7 @@ import torch
 from . import _native
 from .PESQ import PESQ
 from .STOI import STOI
-from .base import BaseMetric, as_rows, check_row_rate, device_lengths, noisy_shape
+from .base import BaseMetric, as_rows, check_row_rate, device_lengths, noisy_shape, same_device
 
 
 _KEYS = ("PESQ", "STOI", "ESTOI")
@@ -74,6 +74,7 @@ class PESQ_STOI(BaseMetric):
         noisy = as_rows(denoised_speech)
         if noisy.shape != clean.shape:
             raise Exception("`clean_speech` and `denoised_speech` should have the same shape.")
+        same_device(clean, noisy)
         B, L = clean.shape
         if not clean.is_cuda:
             mos = self._pesq.scores(clean, noisy, lengths, sample_rate=16000)

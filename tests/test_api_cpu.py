@@ -52,6 +52,25 @@ def test_shape_mismatch_raises_like_reference():
             m(torch.zeros(2, 16000), torch.zeros(2, 16001))
 
 
+def test_mixed_devices_raise_before_any_launch():
+    """The engine entries refuse operands on two devices (torch's own ops in the reference do too):
+    a host pointer handed to a kernel would fault the GPU.  A 'meta' tensor stands in for the
+    second device here."""
+    from fast_speech_enhancement_metrics_amd import PESQ, PESQ_STOI, STOI
+    from fast_speech_enhancement_metrics_amd.alignment import time_align, time_align_segments
+    from fast_speech_enhancement_metrics_amd.base import device_lengths
+    c, n = torch.zeros(2, 16000), torch.zeros(2, 16000, device="meta")
+    calls = [lambda: PESQ().scores(c, n), lambda: STOI(10000).scores(c, n), lambda: PESQ_STOI().scores(c, n),
+             lambda: PESQ().frame_disturbances(c, n), lambda: PESQ(time_align="p862").p862_scores(c, n),
+             lambda: time_align(c, n), lambda: time_align_segments(c, n, mode="p862")]
+    for call in calls:
+        with pytest.raises(RuntimeError, match="same device"):
+            call()
+    # per-row lengths are used as given only on the rows' own device
+    lens = torch.full((2,), 100, dtype=torch.int32)
+    assert device_lengths(lens, 2, 16000, "cpu").device.type == "cpu"
+
+
 def test_clean_none_asserts_like_reference():
     from fast_speech_enhancement_metrics_amd import PESQ, STOI
     for m in (PESQ(), STOI()):

@@ -139,6 +139,22 @@ def test_argument_checks(run, dev):
         realign_bad_intervals(run["ct"], run["dt"], a, run["fr1"][:, :, :10], run["nseg"], run["st"], run["sd"])
 
 
+def test_operands_checked_and_moved(run):
+    """Operand shapes are checked before any launch (a short segment table would be read past its
+    end on the GPU); operands held on the host are moved to the rows' device, same results."""
+    ct, dt, a = run["ct"], run["dt"], run["aligned"]
+    fr1, nseg, st, sd = run["fr1"], run["nseg"], run["st"], run["sd"]
+    for args in ((a, fr1, nseg, st[:, :10], sd), (a, fr1, nseg, st, sd[:, :10]), (a, fr1, nseg[:1], st, sd),
+                 (a[:, :100], fr1, nseg, st, sd)):
+        with pytest.raises(ValueError):
+            realign_bad_intervals(ct, dt, *args)
+    with pytest.raises(ValueError):
+        realign_bad_intervals(ct, dt, a, fr1, torch.full_like(nseg, _native.ALIGN_MAX_SEGMENTS + 1), st, sd)
+    nb, bd, second = realign_bad_intervals(ct, dt, a.cpu(), fr1.cpu(), nseg.cpu(), st.cpu(), sd.cpu())
+    assert nb.device == ct.device and second.device == ct.device
+    assert torch.equal(nb, run["nb"]) and torch.equal(bd, run["bd"]) and torch.equal(second, run["second"])
+
+
 def test_random_plans_against_cpu_path(dev):
     """Random plans at 10 s (1-3 jumps of 120-250 ms by 100-380 samples off the row's delay): the
     engine's intervals and delays equal the package's float64 CPU path on >= 80 % of the rows (a
