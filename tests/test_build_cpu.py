@@ -100,3 +100,11 @@ def test_other_target_is_refused_not_rebuilt(monkeypatch):
     with pytest.raises(ImportError, match="built for gfx950"):
         _native._check_build_id()
     assert not calls
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    """No HIP engine -> ImportError from the loader (no CPU fallback behind a GPU metric's back)."""
+    monkeypatch.setattr(_native, "LIB_PATH", str(tmp_path / "libfsem.so"))
+    monkeypatch.setattr(_native, "_lib", None)
+    with pytest.raises(ImportError, match="not built"):
+        _native.load()
